@@ -1,0 +1,229 @@
+"""bench.py — BASELINE.json metric: Mrays/sec at 1080p/256spp (+ achieved GB/s vs HBM peak).
+
+Workload (BASELINE configs[2], the largest single-GPU config): Stanford-Bunny-sized
+procedural stand-in (69,696 triangles; the asset is absent and there is no network)
+inside the reference Cornell box + light, 1920x1080, 256 spp.  A "step" renders one
+1080p/256spp frame per GPU: the step's N frames are cut into 32x32 tiles dealt
+round-robin over the N ranks (one process per GPU), then the tiles are gathered to
+rank 0 (RCCL over xGMI) and assembled — weak scaling, per-GPU work fixed.
+
+value = closest-hit queries actually traced (non-NaN rays, counted on the device by
+an instrumented pass over the same tiles) summed over ranks x steps / max-over-ranks
+wall time of the K timed steps.  Scene/BVH upload and tile lists are resident in HBM
+before timing.  The kernel is launched on torch's current stream so torch.cuda.Event
+pairs time exactly the render launches (roofline.achieved).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scene bunny|sponza|cornell]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/sec at 1080p/256spp + achieved HBM GB/s vs peak, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
+NODE_BYTES, TRI_BYTES, SHADE_BYTES = 64, 48, 32  # algorithmic bytes per unit
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--scene", default="bunny", choices=["bunny", "sponza", "cornell"])
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spp", type=int, default=256)
+    p.add_argument("--tile", type=int, default=32)
+    p.add_argument("--cpu-rows", type=int, default=0, help="rows in the CPU-baseline sample (0 = auto)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def build_scene(w, kind):
+    if kind == "cornell":
+        L, Q, S = w.cornell_scene()
+        return L, Q, S, None
+    return w.mesh_scene(kind)
+
+
+def cpu_baseline(args, scene, rank, world):
+    """The oracle (CPU port, OpenMP) on a bounded row sample of the same workload."""
+    if rank != 0 or world != 1 or args.no_cpu_baseline:
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle as po
+
+    L, Q, S, T = scene
+    osc = po.OracleScene(L, Q, S, T)
+    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cam = po.camera_param(args.width / args.height, args.spp, 0)
+    def run(rows):
+        # rows spread evenly over the frame, full width, same spp/seed as the GPU frame
+        ys = np.linspace(0, args.height - 1, rows).astype(int)
+        t0 = time.perf_counter()
+        traced = 0
+        for y in ys:
+            r = osc.render(cam, args.width, args.height, 0, int(y), args.width, 1, nthreads=cores, want=())
+            traced += int(r["counters"][po.CNT_TRACED])
+        return traced, time.perf_counter() - t0
+
+    rows = args.cpu_rows
+    if not rows:  # calibrate on 2 rows, then size the sample to ~15 s of CPU work
+        tr, dt = run(2)
+        rows = int(min(args.height, max(2, 2 * 15.0 / max(dt, 1e-3))))
+    traced, dt = run(rows)
+    osc.close()
+    return {"value": traced / dt / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
+            "sample": f"oracle (oracle/wgt_oracle.c, OpenMP {cores} threads) on {rows} full-width rows "
+                      f"of the same {args.width}x{args.height}/{args.spp}spp frame (seed 0): {traced} traced "
+                      f"rays in {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    import webgputracer_amd as w
+    from webgputracer_amd import dist as wdist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    W, H, T, spp = args.width, args.height, args.tile, args.spp
+    scene = build_scene(w, args.scene)
+    ctx = w.Context(local)
+    ctx.upload_scene(*scene)
+    info = ctx.scene_info()
+
+    frames = [(j, j) for j in range(world)]  # this step's frames: (frame id, seed)
+    tiles = wdist.shard_tiles(W, H, T, frames, rank, world)
+    n_max = wdist.max_tiles_per_rank(W, H, T, world, world)
+    dev = torch.device("cuda", local)
+    d_tiles = torch.from_numpy(tiles.view(np.uint8).copy()).to(dev)
+    out = torch.zeros((n_max, T, T, 4), dtype=torch.uint8, device=dev)
+    cam = w.camera_param(W / H, spp, 0)  # per-tile seeds override cam.seed
+
+    # instrumented pass (untimed): exact counts for this rank's tiles
+    st = ctx.render_tiles_stats(cam, W, H, T, T, d_tiles.data_ptr(), len(tiles))
+
+    # a real (non-NULL) stream: the launch, the events and the gather are ordered on it
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+
+    def step(ev):
+        if ev is not None:
+            ev[0].record(stream)
+        ctx.render_tiles_async(cam, W, H, T, T, d_tiles.data_ptr(), len(tiles), d_u8=out.data_ptr(),
+                               stream=stream.cuda_stream)
+        if ev is not None:
+            ev[1].record(stream)
+        bufs = wdist.gather_tiles(out, rank, world, dist)
+        if rank == 0:
+            if world == 1:
+                img = wdist.assemble(tiles, out, W, H, T, [0], xp=torch)
+            else:
+                all_tiles = [wdist.pad_tiles(wdist.shard_tiles(W, H, T, frames, r, world), n_max)
+                             for r in range(world)]
+                img = wdist.assemble(np.concatenate(all_tiles), torch.cat(bufs), W, H, T,
+                                     [f for f, _ in frames], xp=torch)
+            return img
+        return None
+
+    for _ in range(args.warmup):
+        step(None)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if args.steps else 0.0
+
+    mine = np.array([elapsed, st["traced_rays"], st["queries"], st["samples"], st["node_visits"],
+                     st["tri_tests"], kern_ms], np.float64)
+    if world > 1:
+        tm = torch.tensor(mine, device=dev)
+        allv = [torch.zeros_like(tm) for _ in range(world)]
+        dist.all_gather(allv, tm)
+        allv = np.stack([a.cpu().numpy() for a in allv])
+    else:
+        allv = mine[None]
+    max_t = float(allv[:, 0].max())
+    traced = float(allv[:, 1].sum()) * args.steps
+    queries = float(allv[:, 2].sum()) * args.steps
+    samples = float(allv[:, 3].sum()) * args.steps
+    value = traced / max_t / 1e6
+
+    base = cpu_baseline(args, scene, rank, world)
+    if rank == 0:
+        # dominant kernel = k_render<true,false>; algorithmic bytes of rank 0's launch
+        bytes_launch = (mine[4] * NODE_BYTES + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
+        achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+        traffic = None
+        try:
+            with open(args.traffic_json) as f:
+                tj = json.load(f)
+            if tj.get("workload") == f"{args.scene}-{W}x{H}-{spp}spp" and tj.get("n_gpus", 1) == 1 and world == 1:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        n_tris = info["n_tris"]
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(max_t / max(args.steps, 1) * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": f"synthetic: procedural {args.scene} stand-in ({n_tris} tris) in the reference Cornell box"
+                    if args.scene != "cornell" else "synthetic: reference Cornell box",
+            "config": {"workload": f"{args.scene}-{W}x{H}-{spp}spp", "width": W, "height": H, "spp": spp,
+                       "triangles": n_tris, "bvh_nodes": info["bvh_nodes"], "tile": T,
+                       "frames_per_step": world, "parallelism": f"tiles{world}+rccl-gather"},
+            "samples_per_s": round(samples / max_t, 1),
+            "reference_queries_per_s": round(queries / max_t, 1),
+            "kernel_ms": round(kern_ms, 3),
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
+            "cpu_baseline": base,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,121 @@
+"""ctypes binding of libwgt.so — the C-ABI declared in include/wgt_api.h.
+
+The product has no CPU fallback: if libwgt.so is missing, loading fails loudly;
+if no HIP device is present, wgt_create returns an error.  Build with
+`python -c "import __graft_entry__ as g; g.build()"` or `make -C webgputracer_amd`.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "libwgt.so")
+
+# Byte layouts of include/wgt_api.h (= the reference GPU buffers)
+QUAD_DTYPE = np.dtype([("pos", "<f4", 4), ("right", "<f4", 4), ("up", "<f4", 4), ("norm", "<f4", 4),
+                       ("w", "<f4", 3), ("d", "<f4"), ("col", "<f4", 3), ("emissive", "<f4")])
+SPHERE_DTYPE = np.dtype([("center", "<f4", 3), ("radius", "<f4"), ("col", "<f4", 3), ("emissive", "<f4")])
+TRI_DTYPE = np.dtype([("v0", "<f4", 4), ("e1", "<f4", 4), ("e2", "<f4", 4), ("face_norm", "<f4", 4),
+                      ("col", "<f4", 3), ("emissive", "<f4")])
+CAMERA_DTYPE = np.dtype([("origin", "<f4", 3), ("pad0", "<f4"), ("target", "<f4", 3), ("pad1", "<f4"),
+                         ("aspect", "<f4"), ("fovy", "<f4"), ("spp", "<u4"), ("seed", "<u4")])
+TILE_DTYPE = np.dtype([("x0", "<u4"), ("y0", "<u4"), ("seed", "<u4"), ("frame", "<u4")])
+assert QUAD_DTYPE.itemsize == 96 and SPHERE_DTYPE.itemsize == 32
+assert TRI_DTYPE.itemsize == 80 and CAMERA_DTYPE.itemsize == 48 and TILE_DTYPE.itemsize == 16
+
+WGT_OK, WGT_E_INVALID, WGT_E_HIP, WGT_E_NOSCENE, WGT_E_IO, WGT_E_NOMEM = 0, -1, -2, -3, -4, -5
+NO_HIT = 0xFFFFFFFF
+
+
+class WgtStats(ctypes.Structure):
+    _fields_ = [("queries", ctypes.c_uint64), ("traced_rays", ctypes.c_uint64), ("samples", ctypes.c_uint64),
+                ("nan_rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64),
+                ("pixels", ctypes.c_uint64), ("reserved", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
+                ("pad", ctypes.c_float * 3)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k not in ("pad", "reserved")}
+
+
+class WgtSceneInfo(ctypes.Structure):
+    _fields_ = [("n_lights", ctypes.c_uint32), ("n_quads", ctypes.c_uint32), ("n_spheres", ctypes.c_uint32),
+                ("n_tris", ctypes.c_uint32), ("bvh_nodes", ctypes.c_uint32), ("bvh_leaves", ctypes.c_uint32),
+                ("bvh_max_depth", ctypes.c_uint32), ("bvh_max_leaf", ctypes.c_uint32),
+                ("device_bytes", ctypes.c_uint64), ("sah_cost", ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+# Every symbol include/wgt_api.h declares (checked by tests/test_abi.py).
+EXPORTS = [
+    "wgt_create", "wgt_destroy", "wgt_last_error", "wgt_version", "wgt_device_count",
+    "wgt_upload_scene", "wgt_scene_info_get", "wgt_render_tile", "wgt_render_tiles_async",
+    "wgt_render_tiles_stats", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_stream",
+    "wgt_scene_cornell", "wgt_make_triangles", "wgt_load_obj", "wgt_procedural_mesh",
+    "wgt_write_obj", "wgt_write_png",
+]
+
+_lib = None
+
+
+class WgtError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"wgt error {code}: {msg}")
+        self.code = code
+
+
+def lib():
+    """Load libwgt.so (raises if it was not built: there is no fallback path)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} not built; run __graft_entry__.build() (no CPU fallback exists)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, U32, I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "wgt_create": (I, [I, ctypes.POINTER(P)]),
+        "wgt_destroy": (None, [P]),
+        "wgt_last_error": (ctypes.c_char_p, [P]),
+        "wgt_version": (I, []),
+        "wgt_device_count": (I, [ctypes.POINTER(I)]),
+        "wgt_upload_scene": (I, [P, P, U32, P, U32, P, U32, P, U32]),
+        "wgt_scene_info_get": (I, [P, ctypes.POINTER(WgtSceneInfo)]),
+        "wgt_render_tile": (I, [P, P, U32, U32, U32, U32, U32, U32, P, P, P, P]),
+        "wgt_render_tiles_async": (I, [P, P, U32, U32, U32, U32, P, U32, P, P, P, P]),
+        "wgt_render_tiles_stats": (I, [P, P, U32, U32, U32, U32, P, U32, P]),
+        "wgt_trace_rays": (I, [P, P, U32, P, P]),
+        "wgt_trace_rays_async": (I, [P, P, U32, P, P, P]),
+        "wgt_sync": (I, [P]),
+        "wgt_stream": (P, [P]),
+        "wgt_scene_cornell": (I, [P, ctypes.POINTER(U32), P, ctypes.POINTER(U32), P, ctypes.POINTER(U32)]),
+        "wgt_make_triangles": (I, [P, U32, P, I, P, P]),
+        "wgt_load_obj": (I, [ctypes.c_char_p, P, P, I, P, ctypes.POINTER(U32)]),
+        "wgt_procedural_mesh": (I, [I, U32, U32, P, ctypes.POINTER(U32)]),
+        "wgt_write_obj": (I, [ctypes.c_char_p, P, U32]),
+        "wgt_write_png": (I, [ctypes.c_char_p, P, U32, U32]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def ptr(a):
+    """Host numpy array -> void* (None passes NULL)."""
+    if a is None:
+        return None
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def check(rc, ctx=None):
+    if rc != WGT_OK:
+        msg = lib().wgt_last_error(ctx)
+        raise WgtError(rc, msg.decode() if msg else "")
+    return rc

@@ -1,0 +1,238 @@
+// bvh.cpp — binned-SAH BVH2 builder.  Leaf boxes are unions of the padded
+// triangle boxes of the geometry spec (wgt_geom.h tri_box, evaluated on the host
+// with the same fp32 operations), so every node box contains, bit for bit, the
+// boxes of all triangles below it: the traversal is exact.
+#include "bvh.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <limits>
+
+#include "../wgt_geom.h"
+
+namespace wgt {
+namespace {
+
+struct Box {
+  float lo[3], hi[3];
+  void reset() {
+    for (int c = 0; c < 3; ++c) {
+      lo[c] = std::numeric_limits<float>::infinity();
+      hi[c] = -std::numeric_limits<float>::infinity();
+    }
+  }
+  void grow(const Box& b) {
+    for (int c = 0; c < 3; ++c) {
+      lo[c] = std::min(lo[c], b.lo[c]);
+      hi[c] = std::max(hi[c], b.hi[c]);
+    }
+  }
+  double area() const {
+    double dx = (double)hi[0] - lo[0], dy = (double)hi[1] - lo[1], dz = (double)hi[2] - lo[2];
+    if (dx < 0 || dy < 0 || dz < 0) return 0.0;
+    return 2.0 * (dx * dy + dy * dz + dz * dx);
+  }
+};
+
+struct Prim {
+  Box b;
+  float c[3];
+  uint32_t idx;
+};
+
+constexpr int kBins = 32;
+constexpr double kCostTrav = 1.0;
+constexpr double kCostTri = 1.0;
+
+class Builder {
+ public:
+  Builder(std::vector<Prim>& p, BvhOut& o, uint32_t limit) : prims_(p), out_(o), limit_(limit) {}
+
+  // Returns the child reference of the subtree over prims_[begin, end).
+  int Build(uint32_t begin, uint32_t end, uint32_t depth, Box& box) {
+    box.reset();
+    Box cb;
+    cb.reset();
+    for (uint32_t i = begin; i < end; ++i) {
+      box.grow(prims_[i].b);
+      for (int c = 0; c < 3; ++c) {
+        cb.lo[c] = std::min(cb.lo[c], prims_[i].c[c]);
+        cb.hi[c] = std::max(cb.hi[c], prims_[i].c[c]);
+      }
+    }
+    const uint32_t count = end - begin;
+    out_.max_depth = std::max(out_.max_depth, depth);
+    if (count == 1) return MakeLeaf(begin, count, box);
+
+    uint32_t mid = begin;
+    bool median = depth + 24 >= limit_;
+    if (!median) {
+      double best = std::numeric_limits<double>::infinity();
+      int best_axis = -1, best_bin = -1;
+      const double parea = box.area();
+      for (int axis = 0; axis < 3; ++axis) {
+        const float ext = cb.hi[axis] - cb.lo[axis];
+        if (!(ext > 0.0f)) continue;
+        Box bb[kBins];
+        uint32_t bn[kBins] = {};
+        for (auto& b : bb) b.reset();
+        const double scale = kBins / (double)ext;
+        for (uint32_t i = begin; i < end; ++i) {
+          int k = std::min(kBins - 1, (int)((prims_[i].c[axis] - cb.lo[axis]) * scale));
+          bb[k].grow(prims_[i].b);
+          bn[k]++;
+        }
+        double rarea[kBins];
+        uint32_t rcount[kBins];
+        Box acc;
+        acc.reset();
+        uint32_t n = 0;
+        for (int k = kBins - 1; k > 0; --k) {
+          acc.grow(bb[k]);
+          n += bn[k];
+          rarea[k] = acc.area();
+          rcount[k] = n;
+        }
+        acc.reset();
+        n = 0;
+        for (int k = 0; k < kBins - 1; ++k) {
+          acc.grow(bb[k]);
+          n += bn[k];
+          if (n == 0 || rcount[k + 1] == 0) continue;
+          double cost = acc.area() * n + rarea[k + 1] * rcount[k + 1];
+          if (cost < best) {
+            best = cost;
+            best_axis = axis;
+            best_bin = k;
+          }
+        }
+      }
+      const double split_cost = kCostTrav + kCostTri * (parea > 0 ? best / parea : 0.0);
+      const double leaf_cost = kCostTri * count;
+      if (best_axis >= 0 && !(count <= (uint32_t)kLeafMax && leaf_cost <= split_cost)) {
+        const float ext = cb.hi[best_axis] - cb.lo[best_axis];
+        const double scale = kBins / (double)ext;
+        auto it = std::partition(prims_.begin() + begin, prims_.begin() + end, [&](const Prim& p) {
+          int k = std::min(kBins - 1, (int)((p.c[best_axis] - cb.lo[best_axis]) * scale));
+          return k <= best_bin;
+        });
+        mid = (uint32_t)(it - prims_.begin());
+        if (mid == begin || mid == end) median = true;
+      } else if (count <= (uint32_t)kLeafMax) {
+        return MakeLeaf(begin, count, box);
+      } else {
+        median = true;
+      }
+    }
+    if (median) {
+      if (count <= (uint32_t)kLeafMax && depth + 2 >= limit_) return MakeLeaf(begin, count, box);
+      int axis = 0;
+      for (int c = 1; c < 3; ++c)
+        if (cb.hi[c] - cb.lo[c] > cb.hi[axis] - cb.lo[axis]) axis = c;
+      mid = begin + count / 2;
+      std::nth_element(prims_.begin() + begin, prims_.begin() + mid, prims_.begin() + end,
+                       [axis](const Prim& a, const Prim& b) {
+                         return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.idx < b.idx);
+                       });
+    }
+    const uint32_t id = (uint32_t)(out_.nodes.size() / 16);
+    out_.nodes.resize(out_.nodes.size() + 16);
+    Box bl, br;
+    const int rl = Build(begin, mid, depth + 1, bl);
+    const int rr = Build(mid, end, depth + 1, br);
+    WriteNode(id, bl, rl, br, rr);
+    out_.sah_cost += kCostTrav * box.area();
+    return (int)id;
+  }
+
+  void WriteNode(uint32_t id, const Box& b0, int r0, const Box& b1, int r1) {
+    float* n = &out_.nodes[(size_t)id * 16];
+    n[0] = b0.lo[0]; n[1] = b0.hi[0]; n[2] = b0.lo[1]; n[3] = b0.hi[1];
+    n[4] = b1.lo[0]; n[5] = b1.hi[0]; n[6] = b1.lo[1]; n[7] = b1.hi[1];
+    n[8] = b0.lo[2]; n[9] = b0.hi[2]; n[10] = b1.lo[2]; n[11] = b1.hi[2];
+    std::memcpy(&n[12], &r0, 4);
+    std::memcpy(&n[13], &r1, 4);
+    n[14] = 0.0f;
+    n[15] = 0.0f;
+  }
+
+ private:
+  int MakeLeaf(uint32_t begin, uint32_t count, const Box& box) {
+    out_.n_leaves++;
+    out_.max_leaf = std::max(out_.max_leaf, count);
+    out_.sah_cost += kCostTri * count * box.area();
+    return leaf_ref(begin, count);
+  }
+
+  std::vector<Prim>& prims_;
+  BvhOut& out_;
+  uint32_t limit_;
+};
+
+}  // namespace
+
+bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, BvhOut& out,
+              std::string& err) {
+  out = BvhOut{};
+  if (n == 0) { err = "BuildBvh: no triangles"; return false; }
+  if (n >= (1u << 28)) { err = "BuildBvh: too many triangles (max 2^28-1)"; return false; }
+  std::vector<Prim> prims(n);
+  for (uint32_t i = 0; i < n; ++i) {
+    const wgt_triangle& t = tris[i];
+    f3 lo, hi;
+    tri_box(f3{t.v0[0], t.v0[1], t.v0[2]}, f3{t.e1[0], t.e1[1], t.e1[2]},
+            f3{t.e2[0], t.e2[1], t.e2[2]}, lo, hi);
+    Prim& p = prims[i];
+    p.b.lo[0] = lo.x; p.b.lo[1] = lo.y; p.b.lo[2] = lo.z;
+    p.b.hi[0] = hi.x; p.b.hi[1] = hi.y; p.b.hi[2] = hi.z;
+    for (int c = 0; c < 3; ++c) p.c[c] = 0.5f * p.b.lo[c] + 0.5f * p.b.hi[c];
+    p.idx = i;
+    for (int c = 0; c < 3; ++c) {
+      if (!std::isfinite(p.b.lo[c]) || !std::isfinite(p.b.hi[c])) {
+        err = "BuildBvh: non-finite triangle " + std::to_string(i);
+        return false;
+      }
+    }
+  }
+  out.nodes.reserve((size_t)16 * 2 * (n / 2 + 1));
+  Builder b(prims, out, max_depth_limit);
+  Box root_box;
+  const int root = b.Build(0, n, 0, root_box);
+  if (root < 0) {
+    // single leaf: a root node whose second child can never be hit (NaN box:
+    // every slab comparison is false).
+    out.nodes.assign(16, 0.0f);
+    Box nanbox;
+    for (int c = 0; c < 3; ++c) nanbox.lo[c] = nanbox.hi[c] = std::numeric_limits<float>::quiet_NaN();
+    b.WriteNode(0, root_box, root, nanbox, root);
+    out.max_depth = 1;
+  }
+  if (out.max_depth > max_depth_limit) {
+    err = "BuildBvh: depth " + std::to_string(out.max_depth) + " exceeds " +
+          std::to_string(max_depth_limit);
+    return false;
+  }
+  out.n_nodes = (uint32_t)(out.nodes.size() / 16);
+  const double ra = root_box.area();
+  if (ra > 0) out.sah_cost /= ra;
+  out.tris.resize((size_t)n * 12);
+  for (uint32_t i = 0; i < n; ++i) {
+    const wgt_triangle& t = tris[prims[i].idx];
+    float* o = &out.tris[(size_t)i * 12];
+    o[0] = t.v0[0]; o[1] = t.v0[1]; o[2] = t.v0[2];
+    std::memcpy(&o[3], &prims[i].idx, 4);
+    o[4] = t.e1[0]; o[5] = t.e1[1]; o[6] = t.e1[2]; o[7] = 0.0f;
+    o[8] = t.e2[0]; o[9] = t.e2[1]; o[10] = t.e2[2]; o[11] = 0.0f;
+  }
+  out.tshade.resize((size_t)n * 8);
+  for (uint32_t i = 0; i < n; ++i) {
+    const wgt_triangle& t = tris[i];
+    float* o = &out.tshade[(size_t)i * 8];
+    o[0] = t.face_norm[0]; o[1] = t.face_norm[1]; o[2] = t.face_norm[2]; o[3] = t.emissive;
+    o[4] = t.col[0]; o[5] = t.col[1]; o[6] = t.col[2]; o[7] = 0.0f;
+  }
+  return true;
+}
+
+}  // namespace wgt

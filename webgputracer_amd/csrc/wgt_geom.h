@@ -1,0 +1,95 @@
+// wgt_geom.h — triangle / BVH geometry spec shared by the HIP kernels and the
+// host BVH builder.  The reference shader has no triangles or
+// BVH; its host code prepares exactly the Moller-Trumbore inputs
+// v0, e1 = v1 - v0, e2 = v2 - v0 (src/objects/triangle.cpp:9-11), which are
+// what the kernel consumes.
+//
+// Spec: a triangle is hit at t iff Moller-Trumbore passes with t in
+// [kRayMin, kRayMax] AND t lies inside the slab interval of the triangle's own
+// padded box (tri_box).  The closest triangle is the minimum (t, index).  Node
+// boxes are unions of tri boxes and use the same slab formula, so node tests
+// are conservative bit-for-bit (rounding is monotone) and BVH traversal returns
+// exactly the brute-force answer.
+#pragma once
+
+#include "wgt_math.h"
+
+namespace wgt {
+
+// Padded box of one triangle: bounds of v0, v0+e1, v0+e2, then
+// pad = ((hi-lo)*1e-4 + (|lo|+|hi|)*1e-5) + 1e-6 per axis.
+WGT_HD void tri_box(f3 v0, f3 e1, f3 e2, f3& lo, f3& hi) {
+  float l[3], h[3];
+  const float a3[3] = {v0.x, v0.y, v0.z};
+  const float b3[3] = {e1.x, e1.y, e1.z};
+  const float d3[3] = {e2.x, e2.y, e2.z};
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    float a = a3[c];
+    float b = a + b3[c];
+    float d = a + d3[c];
+    float mn = a < b ? a : b;
+    mn = mn < d ? mn : d;
+    float mx = a > b ? a : b;
+    mx = mx > d ? mx : d;
+    float pad = ((mx - mn) * 1e-4f + (fabs_w(mn) + fabs_w(mx)) * 1e-5f) + 1e-6f;
+    l[c] = mn - pad;
+    h[c] = mx + pad;
+  }
+  lo = f3{l[0], l[1], l[2]};
+  hi = f3{h[0], h[1], h[2]};
+}
+
+// 1/d with |d| < 1e-30 replaced by copysign(1e-30, d): finite, so slab values are never NaN.
+WGT_HD float safe_inv(float x) {
+  if (fabs_w(x) < 1e-30f) x = __builtin_copysignf(1e-30f, x);
+  return 1.0f / x;
+}
+
+// Slab interval of box [lo, hi] for origin o and inverse direction inv.
+WGT_HD void slab(f3 o, f3 inv, f3 lo, f3 hi, float& tnear, float& tfar) {
+  float t0x = (lo.x - o.x) * inv.x, t1x = (hi.x - o.x) * inv.x;
+  float t0y = (lo.y - o.y) * inv.y, t1y = (hi.y - o.y) * inv.y;
+  float t0z = (lo.z - o.z) * inv.z, t1z = (hi.z - o.z) * inv.z;
+  float nx = t0x < t1x ? t0x : t1x, fx = t0x < t1x ? t1x : t0x;
+  float ny = t0y < t1y ? t0y : t1y, fy = t0y < t1y ? t1y : t0y;
+  float nz = t0z < t1z ? t0z : t1z, fz = t0z < t1z ? t1z : t0z;
+  float n = ny > nx ? ny : nx;
+  n = nz > n ? nz : n;
+  float f = fy < fx ? fy : fx;
+  f = fz < f ? fz : f;
+  tnear = n;
+  tfar = f;
+}
+
+// Two-sided Moller-Trumbore (fixed op order).
+WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {
+  f3 pvec = cross(d, e2);
+  float det = dot(e1, pvec);
+  if (fabs_w(det) < 1e-12f) return false;
+  float inv_det = 1.0f / det;
+  f3 tvec = o - v0;
+  float u = dot(tvec, pvec) * inv_det;
+  if (u < 0.0f || u > 1.0f) return false;
+  f3 qvec = cross(tvec, e1);
+  float v = dot(d, qvec) * inv_det;
+  if (v < 0.0f || u + v > 1.0f) return false;
+  float t = dot(e2, qvec) * inv_det;
+  if (t < kRayMin || kRayMax < t) return false;
+  tout = t;
+  return true;
+}
+
+// BVH2 node, 64 B (4 x float4):
+//   a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
+//   b = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
+//   c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
+//   d = (ref0, ref1, -, -) as int bits
+// child ref >= 0: internal node index; < 0: leaf, ~ref = first*8 + (count-1)
+// into the leaf-ordered triangle array (count <= 8).
+constexpr int kLeafMax = 8;
+WGT_HD int leaf_ref(uint32_t first, uint32_t count) { return ~(int)(first * 8u + (count - 1u)); }
+WGT_HD uint32_t leaf_first(int ref) { return ((uint32_t)~ref) >> 3; }
+WGT_HD uint32_t leaf_count(int ref) { return (((uint32_t)~ref) & 7u) + 1u; }
+
+}  // namespace wgt

@@ -1,0 +1,71 @@
+// wgt_internal.h — device-side data layout shared by the kernel TU and the
+// runtime TU (not part of the public ABI).
+//
+// HBM layout of a scene:
+//   quads   : lights then quads, 96-B reference records (6 x float4) — read with
+//             wave-uniform (scalar) loads, 1.7 KB for the Cornell box
+//   spheres : 32-B reference records (2 x float4)
+//   nodes   : BVH2 nodes, 64 B (4 x float4), root = node 0, see wgt_geom.h
+//   tris    : leaf-ordered Moller-Trumbore records, 48 B (3 x float4):
+//             (v0.xyz, original index bits), (e1.xyz, 0), (e2.xyz, 0)
+//   tshade  : per ORIGINAL triangle, 32 B: (face_norm.xyz, emissive), (col.xyz, 0)
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/wgt_api.h"
+
+namespace wgt {
+
+constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
+constexpr int kStackLds = 32;     // per-lane traversal stack entries in LDS
+constexpr int kStackScratch = 64; // overflow entries in private (scratch) memory
+constexpr int kMaxBvhDepth = kStackLds + kStackScratch - 2;
+
+struct DevScene {
+  const float4* __restrict__ quads;   // n_lights + n_quads records
+  const float4* __restrict__ spheres; // n_spheres records
+  const float4* __restrict__ nodes;
+  const float4* __restrict__ tris;
+  const float4* __restrict__ tshade;
+  uint32_t n_lights, n_quads, n_spheres, n_tris;
+  uint32_t n_nodes;
+  uint32_t last_sphere_emissive;
+  float light_area;  // length(cross(lights[0].right, lights[0].up)) (path_tracer.wgsl:205)
+  uint32_t max_iters; // traversal safety bound (2 x nodes + 2)
+};
+
+// Per-frame camera constants of setup_camera_ray (path_tracer.wgsl:239-262),
+// computed once on the host with the same fp32 operations (wgt_math.h).
+struct DevFrame {
+  float ox, oy, oz;    // origin
+  float pox, poy, poz; // pixel_origin
+  float dux, duy, duz; // pixel_delta_u
+  float dvx, dvy, dvz; // pixel_delta_v
+  float recip_sqrt_spp;
+  float fspp;          // f32(camera.spp)
+  uint32_t sqrt_spp;
+  uint32_t W, H;
+  uint32_t tw, th, n_tiles;
+};
+
+enum {
+  CNT_QUERIES = 0,
+  CNT_TRACED,
+  CNT_SAMPLES,
+  CNT_NAN,
+  CNT_NODES,
+  CNT_TRIS,
+  CNT_PIXELS,
+  CNT_N = 8
+};
+
+// Launchers implemented in wgt_kernels.hip
+hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
+                         uchar4* out8, float4* out32, uint32_t* outhit,
+                         unsigned long long* counters, hipStream_t stream);
+hipError_t launch_trace(const DevScene& sc, const float* d_rays, uint32_t n, uint32_t* prim,
+                        float* dist, hipStream_t stream);
+
+}  // namespace wgt

@@ -1,0 +1,143 @@
+// wgt_math.h — fp32 vector math + the numerics contract of the product path.
+//
+// Used by the HIP kernels (device) and by the host scene/camera code, so that a
+// value computed on either side has the same bits.  Everything here is plain
+// IEEE fp32 +,-,*,/,sqrt with NO contraction (the library is built with
+// -ffp-contract=off) and a fixed left-to-right evaluation order that restates
+// the WGSL expressions of resources/shader/path_tracer.wgsl (reference).
+//
+// WGSL leaves transcendental precision to the implementation; the product fixes
+// it here: Cody-Waite reduction by pi/2 with a 17+24-bit split
+// and degree-9/8 minimax polynomials, built from +,-,*,floor only.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define WGT_HD __host__ __device__ __forceinline__
+
+namespace wgt {
+
+// path_tracer.wgsl:1-10
+constexpr float kPI = 3.14159265359f;
+constexpr float k_1_PI = 0.318309886184f;
+constexpr uint32_t kNoHit = 0xffffffffu;
+constexpr int kRayDepth = 50;
+constexpr float kRayMin = 0.001f;
+constexpr float kRayMax = 1e20f;
+
+struct f3 {
+  float x, y, z;
+};
+
+WGT_HD f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+WGT_HD f3 operator+(f3 a, f3 b) { return f3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+WGT_HD f3 operator-(f3 a, f3 b) { return f3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+WGT_HD f3 operator-(f3 a) { return f3{-a.x, -a.y, -a.z}; }
+WGT_HD f3 operator*(f3 a, f3 b) { return f3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+WGT_HD f3 operator*(float s, f3 a) { return f3{s * a.x, s * a.y, s * a.z}; }
+WGT_HD f3 operator/(f3 a, float s) { return f3{a.x / s, a.y / s, a.z / s}; }
+// WGSL dot: (x*x + y*y) + z*z
+WGT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+WGT_HD f3 cross(f3 a, f3 b) {
+  return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+WGT_HD float length(f3 a) { return __builtin_sqrtf(dot(a, a)); }
+// WGSL normalize(v) = v / length(v)   (zero vector -> NaN, as the reference relies on)
+WGT_HD f3 normalize(f3 a) { return a / length(a); }
+WGT_HD float distance(f3 a, f3 b) { return length(a - b); }
+WGT_HD bool has_nan(f3 a) { return (a.x != a.x) | (a.y != a.y) | (a.z != a.z); }
+
+// path_tracer.wgsl:68-70
+WGT_HD float fabs_w(float x) { return x < 0.0f ? -x : x; }
+// WGSL sign()
+WGT_HD float sign_w(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+// WGSL max(x, 0.0) with max(NaN, 0) = 0
+WGT_HD float max0(float x) { return x > 0.0f ? x : 0.0f; }
+
+// ---------------------------------------------------------------- transcendental
+namespace detail {
+constexpr float k2OverPi = 0.636619772367581343f;
+constexpr float kPio2Hi = 1.5707855225e+00f;  // 0x3fc90f80 (17 significant bits)
+constexpr float kPio2Lo = 1.0804334124e-05f;  // 0x37354443
+WGT_HD float reduce(float x, float& q) {
+  float k = __builtin_floorf(x * k2OverPi + 0.5f);
+  q = k - 4.0f * __builtin_floorf(k * 0.25f);
+  return (x - k * kPio2Hi) - k * kPio2Lo;
+}
+WGT_HD float ksin(float r) {
+  float z = r * r;
+  return r + (r * z) * (-1.6666667163e-01f +
+                        z * (8.3333337680e-03f + z * (-1.9841270114e-04f + z * 2.7557314297e-06f)));
+}
+WGT_HD float kcos(float r) {
+  float z = r * r;
+  return (1.0f - 0.5f * z) +
+         (z * z) * (4.1666667908e-02f +
+                    z * (-1.3888889225e-03f + z * (2.4801587642e-05f + z * -2.7557314297e-07f)));
+}
+}  // namespace detail
+
+WGT_HD float sin_w(float x) {
+  float q;
+  float r = detail::reduce(x, q);
+  if (q == 0.0f) return detail::ksin(r);
+  if (q == 1.0f) return detail::kcos(r);
+  if (q == 2.0f) return -detail::ksin(r);
+  return -detail::kcos(r);
+}
+WGT_HD float cos_w(float x) {
+  float q;
+  float r = detail::reduce(x, q);
+  if (q == 0.0f) return detail::kcos(r);
+  if (q == 1.0f) return -detail::ksin(r);
+  if (q == 2.0f) return -detail::kcos(r);
+  return detail::ksin(r);
+}
+// sin and cos of the same angle with one reduction (bit-identical to sin_w/cos_w)
+WGT_HD void sincos_w(float x, float& s, float& c) {
+  float q;
+  float r = detail::reduce(x, q);
+  float ks = detail::ksin(r), kc = detail::kcos(r);
+  if (q == 0.0f) { s = ks; c = kc; }
+  else if (q == 1.0f) { s = kc; c = -ks; }
+  else if (q == 2.0f) { s = -ks; c = -kc; }
+  else { s = -kc; c = ks; }
+}
+WGT_HD float tan_w(float x) { return sin_w(x) / cos_w(x); }
+WGT_HD float radians_w(float deg) { return deg * 0.017453292519943295f; }
+
+// ------------------------------------------------------------------- rand()
+// path_tracer.wgsl:88-95.  bitcast<f32>(0x2f800004u) = 2.3283075e-10 (> 2^-32).
+constexpr float kRandScale = __builtin_bit_cast(float, 0x2f800004u);
+WGT_HD float rand_next(uint32_t& seed) {
+  uint32_t s = seed * 747796405u + 2891336453u;
+  seed = s;
+  uint32_t word = ((s >> ((s >> 28u) + 4u)) ^ s) * 277803737u;
+  return (float)((word >> 22u) ^ word) * kRandScale;
+}
+// Advance the LCG state by n steps (n < 256) in 8 affine compositions; used to
+// skip the remaining bounces of a NaN-absorbed path bit-exactly.
+struct Affine {
+  uint32_t a, c;
+};
+struct AffinePow2 {
+  Affine f[8];
+  constexpr AffinePow2() : f{} {
+    Affine g{747796405u, 2891336453u};
+    for (int j = 0; j < 8; ++j) {
+      f[j] = g;
+      g = Affine{g.a * g.a, g.a * g.c + g.c};
+    }
+  }
+};
+WGT_HD uint32_t lcg_jump(uint32_t s, uint32_t n) {
+  constexpr AffinePow2 P{};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    if ((n >> j) & 1u) s = P.f[j].a * s + P.f[j].c;
+  }
+  return s;
+}
+
+}  // namespace wgt

@@ -1,0 +1,414 @@
+// wgt_runtime.cpp — the C-ABI (include/wgt_api.h) over HIP: device context and
+// stream (replacing Renderer::InitDevice, render.cpp:49-147), scene upload with
+// BVH build (replacing Scene::InitBuffers, scene.cpp:161-165), the render launch
+// (replacing the compute pass of Renderer::OnRender, render.cpp:461-491) and the
+// readback (replacing saveTexture's copyTextureToBuffer + mapAsync,
+// save_texture.h:10-87).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/wgt_api.h"
+#include "host/bvh.h"
+#include "wgt_error.h"
+#include "wgt_geom.h"
+#include "wgt_internal.h"
+
+using namespace wgt;
+
+namespace {
+thread_local std::string g_err;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+}  // namespace
+
+namespace wgt {
+void set_thread_error(const std::string& msg) { g_err = msg; }
+}  // namespace wgt
+
+struct wgt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::string err;
+  bool has_scene = false;
+  DevScene sc{};
+  void* scene_mem = nullptr;
+  wgt_scene_info info{};
+  // scratch for the synchronous entry points
+  DevBuf tiles, out8, out32, hit, counters, rays, prim, dist;
+};
+
+namespace {
+
+int fail(wgt_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  g_err = msg;
+  return code;
+}
+
+#define WGT_HIP(ctx, expr)                                                                    \
+  do {                                                                                        \
+    hipError_t e_ = (expr);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      return fail((ctx), WGT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
+  } while (0)
+
+int ensure(wgt_ctx* ctx, DevBuf& b, size_t bytes) {
+  if (b.bytes >= bytes) return WGT_OK;
+  if (b.p) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(b.p);
+    b.p = nullptr;
+    b.bytes = 0;
+  }
+  size_t want = std::max<size_t>(bytes, 256);
+  WGT_HIP(ctx, hipMalloc(&b.p, want));
+  b.bytes = want;
+  return WGT_OK;
+}
+
+void free_buf(DevBuf& b) {
+  if (b.p) (void)hipFree(b.p);
+  b.p = nullptr;
+  b.bytes = 0;
+}
+
+size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+// setup_camera_ray's frame-invariant terms (path_tracer.wgsl:239-257), same fp32
+// operations as the WGSL per-invocation evaluation.
+DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
+  DevFrame fr{};
+  const float theta = radians_w(cam.fovy);
+  const f3 origin = f3{cam.origin[0], cam.origin[1], cam.origin[2]};
+  const f3 end = f3{cam.target[0], cam.target[1], cam.target[2]};
+  const float focal_length = length(origin - end);
+  const float h = tan_w(theta * 0.5f);
+  const float viewport_height = 2.0f * h * focal_length;
+  const float viewport_width = viewport_height * cam.aspect;
+  const f3 w = normalize(origin - end);
+  const f3 u = normalize(cross(f3{0.0f, 1.0f, 0.0f}, w));
+  const f3 v = cross(w, u);
+  const f3 viewport_u = viewport_width * u;
+  const f3 viewport_v = viewport_height * (-v);
+  const f3 du = viewport_u / (float)W;
+  const f3 dv = viewport_v / (float)H;
+  const f3 vul = ((origin - focal_length * w) - 0.5f * viewport_u) - 0.5f * viewport_v;
+  const f3 po = vul + 0.5f * (du + dv);
+  fr.ox = origin.x; fr.oy = origin.y; fr.oz = origin.z;
+  fr.pox = po.x; fr.poy = po.y; fr.poz = po.z;
+  fr.dux = du.x; fr.duy = du.y; fr.duz = du.z;
+  fr.dvx = dv.x; fr.dvy = dv.y; fr.dvz = dv.z;
+  fr.recip_sqrt_spp = 1.0f / __builtin_sqrtf((float)cam.spp);
+  fr.fspp = (float)cam.spp;
+  fr.sqrt_spp = (uint32_t)__builtin_sqrtf((float)cam.spp);
+  fr.W = W;
+  fr.H = H;
+  return fr;
+}
+
+int check_render_args(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H,
+                      uint32_t tw, uint32_t th) {
+  if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
+  if (!cam) return fail(ctx, WGT_E_INVALID, "null camera");
+  if (!ctx->has_scene) return fail(ctx, WGT_E_NOSCENE, "no scene uploaded");
+  if (W == 0 || H == 0) return fail(ctx, WGT_E_INVALID, "empty frame");
+  if (tw == 0 || th == 0) return fail(ctx, WGT_E_INVALID, "empty tile");
+  if (!(cam->aspect == cam->aspect) || !(cam->fovy == cam->fovy))
+    return fail(ctx, WGT_E_INVALID, "NaN camera parameter");
+  return WGT_OK;
+}
+
+void fill_stats(const unsigned long long* c, wgt_stats* s) {
+  s->queries = c[CNT_QUERIES];
+  s->traced_rays = c[CNT_TRACED];
+  s->samples = c[CNT_SAMPLES];
+  s->nan_rays = c[CNT_NAN];
+  s->node_visits = c[CNT_NODES];
+  s->tri_tests = c[CNT_TRIS];
+  s->pixels = c[CNT_PIXELS];
+}
+
+}  // namespace
+
+extern "C" {
+
+int wgt_version(void) { return WGT_API_VERSION; }
+
+const char* wgt_last_error(const wgt_ctx* ctx) { return ctx ? ctx->err.c_str() : g_err.c_str(); }
+
+int wgt_device_count(int* count) {
+  if (!count) return fail(nullptr, WGT_E_INVALID, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return fail(nullptr, WGT_E_HIP, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+  }
+  *count = n;
+  return WGT_OK;
+}
+
+int wgt_create(int hip_device, wgt_ctx** out) {
+  if (!out) return fail(nullptr, WGT_E_INVALID, "null out");
+  *out = nullptr;
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0)
+    return fail(nullptr, WGT_E_HIP, "no HIP device available (the product has no CPU fallback)");
+  if (hip_device < 0 || hip_device >= n) return fail(nullptr, WGT_E_INVALID, "bad device index");
+  wgt_ctx* ctx = new wgt_ctx();
+  ctx->device = hip_device;
+  auto cleanup = [&](const char* what, hipError_t err) {
+    std::string m = std::string(what) + ": " + hipGetErrorString(err);
+    wgt_destroy(ctx);
+    return fail(nullptr, WGT_E_HIP, m);
+  };
+  if ((e = hipSetDevice(hip_device)) != hipSuccess) return cleanup("hipSetDevice", e);
+  if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess)
+    return cleanup("hipStreamCreate", e);
+  if ((e = hipEventCreate(&ctx->ev0)) != hipSuccess) return cleanup("hipEventCreate", e);
+  if ((e = hipEventCreate(&ctx->ev1)) != hipSuccess) return cleanup("hipEventCreate", e);
+  *out = ctx;
+  return WGT_OK;
+}
+
+void wgt_destroy(wgt_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
+  free_buf(ctx->tiles); free_buf(ctx->out8); free_buf(ctx->out32); free_buf(ctx->hit);
+  free_buf(ctx->counters); free_buf(ctx->rays); free_buf(ctx->prim); free_buf(ctx->dist);
+  if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
+  if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
+  if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+void* wgt_stream(wgt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int wgt_sync(wgt_ctx* ctx) {
+  if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return WGT_OK;
+}
+
+int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, const wgt_quad* quads,
+                     uint32_t n_quads, const wgt_sphere* spheres, uint32_t n_spheres,
+                     const wgt_triangle* tris, uint32_t n_tris) {
+  if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
+  if (n_lights < 1 || !lights)
+    return fail(ctx, WGT_E_INVALID, "need >= 1 light (sample_from_light reads lights[0])");
+  if (n_spheres < 1 || !spheres)
+    return fail(ctx, WGT_E_INVALID, "need >= 1 sphere (the reference binds a dummy sphere)");
+  if (n_quads > 0 && !quads) return fail(ctx, WGT_E_INVALID, "null quads");
+  if (n_tris > 0 && !tris) return fail(ctx, WGT_E_INVALID, "null triangles");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+
+  BvhOut bvh;
+  if (n_tris > 0) {
+    std::string err;
+    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, bvh, err)) return fail(ctx, WGT_E_INVALID, err);
+  }
+  const uint32_t nlq = n_lights + n_quads;
+  const size_t b_quads = align256((size_t)nlq * 96);
+  const size_t b_sph = align256((size_t)n_spheres * 32);
+  const size_t b_nodes = align256(bvh.nodes.size() * 4);
+  const size_t b_tris = align256(bvh.tris.size() * 4);
+  const size_t b_shade = align256(bvh.tshade.size() * 4);
+  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade;
+
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (ctx->scene_mem) {
+    (void)hipFree(ctx->scene_mem);
+    ctx->scene_mem = nullptr;
+  }
+  ctx->has_scene = false;
+  WGT_HIP(ctx, hipMalloc(&ctx->scene_mem, total));
+  char* base = (char*)ctx->scene_mem;
+  std::vector<char> host(total, 0);
+  std::memcpy(host.data(), lights, (size_t)n_lights * 96);
+  if (n_quads) std::memcpy(host.data() + (size_t)n_lights * 96, quads, (size_t)n_quads * 96);
+  std::memcpy(host.data() + b_quads, spheres, (size_t)n_spheres * 32);
+  if (n_tris) {
+    std::memcpy(host.data() + b_quads + b_sph, bvh.nodes.data(), bvh.nodes.size() * 4);
+    std::memcpy(host.data() + b_quads + b_sph + b_nodes, bvh.tris.data(), bvh.tris.size() * 4);
+    std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris, bvh.tshade.data(),
+                bvh.tshade.size() * 4);
+  }
+  WGT_HIP(ctx, hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
+
+  DevScene& sc = ctx->sc;
+  sc = DevScene{};
+  sc.quads = (const float4*)base;
+  sc.spheres = (const float4*)(base + b_quads);
+  sc.nodes = (const float4*)(base + b_quads + b_sph);
+  sc.tris = (const float4*)(base + b_quads + b_sph + b_nodes);
+  sc.tshade = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris);
+  sc.n_lights = n_lights;
+  sc.n_quads = n_quads;
+  sc.n_spheres = n_spheres;
+  sc.n_tris = n_tris;
+  sc.n_nodes = bvh.n_nodes;
+  sc.last_sphere_emissive = spheres[n_spheres - 1].emissive > 0.0f ? 1u : 0u;
+  const f3 lr = f3{lights[0].right[0], lights[0].right[1], lights[0].right[2]};
+  const f3 lu = f3{lights[0].up[0], lights[0].up[1], lights[0].up[2]};
+  sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
+  sc.max_iters = 2u * bvh.n_nodes + 8u;
+
+  wgt_scene_info& in = ctx->info;
+  in = wgt_scene_info{};
+  in.n_lights = n_lights;
+  in.n_quads = n_quads;
+  in.n_spheres = n_spheres;
+  in.n_tris = n_tris;
+  in.bvh_nodes = bvh.n_nodes;
+  in.bvh_leaves = bvh.n_leaves;
+  in.bvh_max_depth = bvh.max_depth;
+  in.bvh_max_leaf = bvh.max_leaf;
+  in.device_bytes = total;
+  in.sah_cost = bvh.sah_cost;
+  ctx->has_scene = true;
+  return WGT_OK;
+}
+
+int wgt_scene_info_get(const wgt_ctx* ctx, wgt_scene_info* info) {
+  if (!ctx || !info) return fail(nullptr, WGT_E_INVALID, "null argument");
+  if (!ctx->has_scene) return fail(const_cast<wgt_ctx*>(ctx), WGT_E_NOSCENE, "no scene uploaded");
+  *info = ctx->info;
+  return WGT_OK;
+}
+
+int wgt_render_tiles_async(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H,
+                           uint32_t tw, uint32_t th, const wgt_tile* d_tiles, uint32_t n_tiles,
+                           void* d_rgba8, float* d_rgba32f, uint32_t* d_hit_id, void* stream) {
+  int rc = check_render_args(ctx, cam, W, H, tw, th);
+  if (rc) return rc;
+  if (n_tiles == 0) return WGT_OK;
+  if (!d_tiles) return fail(ctx, WGT_E_INVALID, "null tile list");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  DevFrame fr = make_frame(*cam, W, H);
+  fr.tw = tw;
+  fr.th = th;
+  fr.n_tiles = n_tiles;
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, (uchar4*)d_rgba8, (float4*)d_rgba32f, d_hit_id,
+                             nullptr, s));
+  return WGT_OK;
+}
+
+int wgt_render_tiles_stats(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H,
+                           uint32_t tw, uint32_t th, const wgt_tile* d_tiles, uint32_t n_tiles,
+                           wgt_stats* stats) {
+  int rc = check_render_args(ctx, cam, W, H, tw, th);
+  if (rc) return rc;
+  if (!stats) return fail(ctx, WGT_E_INVALID, "null stats");
+  std::memset(stats, 0, sizeof *stats);
+  if (n_tiles == 0) return WGT_OK;
+  if (!d_tiles) return fail(ctx, WGT_E_INVALID, "null tile list");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  if ((rc = ensure(ctx, ctx->counters, CNT_N * 8))) return rc;
+  WGT_HIP(ctx, hipMemsetAsync(ctx->counters.p, 0, CNT_N * 8, ctx->stream));
+  DevFrame fr = make_frame(*cam, W, H);
+  fr.tw = tw;
+  fr.th = th;
+  fr.n_tiles = n_tiles;
+  WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, nullptr, nullptr, nullptr,
+                             (unsigned long long*)ctx->counters.p, ctx->stream));
+  unsigned long long c[CNT_N];
+  WGT_HIP(ctx, hipMemcpyAsync(c, ctx->counters.p, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  fill_stats(c, stats);
+  return WGT_OK;
+}
+
+int wgt_render_tile(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H, uint32_t x0,
+                    uint32_t y0, uint32_t tw, uint32_t th, uint8_t* rgba8_out, float* rgba32f_out,
+                    uint32_t* hit_id_out, wgt_stats* stats) {
+  int rc = check_render_args(ctx, cam, W, H, tw, th);
+  if (rc) return rc;
+  if (x0 >= W || y0 >= H) return fail(ctx, WGT_E_INVALID, "tile origin outside the frame");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  const size_t npx = (size_t)tw * th;
+  wgt_tile tile{x0, y0, cam->seed, 0u};
+  if ((rc = ensure(ctx, ctx->tiles, sizeof tile))) return rc;
+  if (rgba8_out && (rc = ensure(ctx, ctx->out8, npx * 4))) return rc;
+  if (rgba32f_out && (rc = ensure(ctx, ctx->out32, npx * 16))) return rc;
+  if (hit_id_out && (rc = ensure(ctx, ctx->hit, npx * 4))) return rc;
+  WGT_HIP(ctx, hipMemcpyAsync(ctx->tiles.p, &tile, sizeof tile, hipMemcpyHostToDevice, ctx->stream));
+  // Pixels of a partially covered tile that fall outside the frame are not written
+  // by the kernel (path_tracer.wgsl:377); give them defined contents.
+  if (x0 + (uint64_t)tw > W || y0 + (uint64_t)th > H) {
+    if (rgba8_out) WGT_HIP(ctx, hipMemsetAsync(ctx->out8.p, 0, npx * 4, ctx->stream));
+    if (rgba32f_out) WGT_HIP(ctx, hipMemsetAsync(ctx->out32.p, 0, npx * 16, ctx->stream));
+    if (hit_id_out) WGT_HIP(ctx, hipMemsetAsync(ctx->hit.p, 0xff, npx * 4, ctx->stream));
+  }
+  DevFrame fr = make_frame(*cam, W, H);
+  fr.tw = tw;
+  fr.th = th;
+  fr.n_tiles = 1;
+  WGT_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
+  WGT_HIP(ctx, launch_render(ctx->sc, fr, (const wgt_tile*)ctx->tiles.p,
+                             rgba8_out ? (uchar4*)ctx->out8.p : nullptr,
+                             rgba32f_out ? (float4*)ctx->out32.p : nullptr,
+                             hit_id_out ? (uint32_t*)ctx->hit.p : nullptr, nullptr, ctx->stream));
+  WGT_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  if (rgba8_out)
+    WGT_HIP(ctx, hipMemcpyAsync(rgba8_out, ctx->out8.p, npx * 4, hipMemcpyDeviceToHost, ctx->stream));
+  if (rgba32f_out)
+    WGT_HIP(ctx, hipMemcpyAsync(rgba32f_out, ctx->out32.p, npx * 16, hipMemcpyDeviceToHost, ctx->stream));
+  if (hit_id_out)
+    WGT_HIP(ctx, hipMemcpyAsync(hit_id_out, ctx->hit.p, npx * 4, hipMemcpyDeviceToHost, ctx->stream));
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (stats) {
+    float ms = 0.0f;
+    WGT_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
+    rc = wgt_render_tiles_stats(ctx, cam, W, H, tw, th, (const wgt_tile*)ctx->tiles.p, 1, stats);
+    if (rc) return rc;
+    stats->kernel_ms = ms;
+  }
+  return WGT_OK;
+}
+
+int wgt_trace_rays_async(wgt_ctx* ctx, const float* d_rays, uint32_t n, uint32_t* d_prim_id,
+                         float* d_dist, void* stream) {
+  if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
+  if (!ctx->has_scene) return fail(ctx, WGT_E_NOSCENE, "no scene uploaded");
+  if (n == 0) return WGT_OK;
+  if (!d_rays || !d_prim_id || !d_dist) return fail(ctx, WGT_E_INVALID, "null buffer");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  WGT_HIP(ctx, launch_trace(ctx->sc, d_rays, n, d_prim_id, d_dist, s));
+  return WGT_OK;
+}
+
+int wgt_trace_rays(wgt_ctx* ctx, const float* rays, uint32_t n, uint32_t* prim_id, float* dist) {
+  if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
+  if (!ctx->has_scene) return fail(ctx, WGT_E_NOSCENE, "no scene uploaded");
+  if (n == 0) return WGT_OK;
+  if (!rays || !prim_id || !dist) return fail(ctx, WGT_E_INVALID, "null buffer");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = ensure(ctx, ctx->rays, (size_t)n * 24))) return rc;
+  if ((rc = ensure(ctx, ctx->prim, (size_t)n * 4))) return rc;
+  if ((rc = ensure(ctx, ctx->dist, (size_t)n * 4))) return rc;
+  WGT_HIP(ctx, hipMemcpyAsync(ctx->rays.p, rays, (size_t)n * 24, hipMemcpyHostToDevice, ctx->stream));
+  WGT_HIP(ctx, launch_trace(ctx->sc, (const float*)ctx->rays.p, n, (uint32_t*)ctx->prim.p,
+                            (float*)ctx->dist.p, ctx->stream));
+  WGT_HIP(ctx, hipMemcpyAsync(prim_id, ctx->prim.p, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  WGT_HIP(ctx, hipMemcpyAsync(dist, ctx->dist.p, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return WGT_OK;
+}
+
+}  // extern "C"

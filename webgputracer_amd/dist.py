@@ -1,0 +1,89 @@
+"""Tile sharding of frames over GPUs + the final gather (RCCL over xGMI).
+
+The reference distributes only whole frame ranges over machines via SSH
+(settings/run.py:11-24: frames 1-320 local, 321-600 remote, no data exchange).
+Here one process per GPU renders an interleaved share of the T x T tiles of a
+batch of frames, and rank 0 gathers the tiles and assembles the frames:
+
+  * pixel (x, y) of frame f depends only on (x, y, W, H, seed_f, scene)
+    (path_tracer.wgsl:378), so ANY partition reproduces the single-GPU frame bit
+    for bit; tiles are dealt round-robin (tile t of frame j -> rank (t + j) % N)
+    so the expensive and the cheap (escaping, NaN-absorbed) regions spread evenly;
+  * weak scaling: a step renders N frames on N GPUs, i.e. one frame's worth of
+    tiles per GPU; the only collective is one gather per step
+    (torch.distributed backend "nccl" = RCCL on ROCm; "gloo" in CPU tests).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import TILE_DTYPE
+
+
+def frame_tiles(W: int, H: int, T: int):
+    """(x0, y0) of every T x T tile of a W x H frame, row-major."""
+    ys, xs = np.meshgrid(np.arange(0, H, T, dtype=np.uint32), np.arange(0, W, T, dtype=np.uint32), indexing="ij")
+    return np.stack([xs.ravel(), ys.ravel()], axis=1)
+
+
+def shard_tiles(W: int, H: int, T: int, frames, rank: int, world: int):
+    """Tile list (TILE_DTYPE) of `rank` for the batch `frames` (list of (frame_id, seed)).
+    Tile t of the j-th frame of the batch goes to rank (t + j) % world."""
+    xy = frame_tiles(W, H, T)
+    out = []
+    for j, (fid, seed) in enumerate(frames):
+        sel = np.nonzero((np.arange(len(xy)) + j) % world == rank)[0]
+        t = np.zeros(len(sel), TILE_DTYPE)
+        t["x0"] = xy[sel, 0]
+        t["y0"] = xy[sel, 1]
+        t["seed"] = seed & 0xFFFFFFFF
+        t["frame"] = fid
+        out.append(t)
+    return np.concatenate(out) if out else np.zeros(0, TILE_DTYPE)
+
+
+def max_tiles_per_rank(W: int, H: int, T: int, n_frames: int, world: int) -> int:
+    n = len(frame_tiles(W, H, T))
+    return max(len(shard_tiles(W, H, T, [(j, j) for j in range(n_frames)], r, world)) for r in range(world))
+
+
+def assemble(tiles: np.ndarray, data, W: int, H: int, T: int, frame_ids, xp=np):
+    """Scatter compact tiles data[k] (T, T, C) of tile list `tiles` into frames.
+    Works with numpy or torch (pass xp=torch and torch tensors)."""
+    C = data.shape[-1]
+    frames = {}
+    for fid in frame_ids:
+        frames[int(fid)] = xp.zeros((H, W, C), dtype=data.dtype) if xp is np else \
+            xp.zeros((H, W, C), dtype=data.dtype, device=data.device)
+    for k in range(len(tiles)):
+        fid = int(tiles["frame"][k])
+        if fid not in frames:
+            continue
+        x0, y0 = int(tiles["x0"][k]), int(tiles["y0"][k])
+        w, h = min(T, W - x0), min(T, H - y0)
+        frames[fid][y0:y0 + h, x0:x0 + w] = data[k, :h, :w]
+    return frames
+
+
+def pad_tiles(tiles: np.ndarray, n: int):
+    """Pad a tile list to n entries (pad tiles have frame = 0xffffffff and are ignored by assemble)."""
+    if len(tiles) >= n:
+        return tiles
+    pad = np.zeros(n - len(tiles), TILE_DTYPE)
+    pad["frame"] = 0xFFFFFFFF
+    if len(tiles):
+        pad["x0"], pad["y0"], pad["seed"] = tiles["x0"][0], tiles["y0"][0], tiles["seed"][0]
+    return np.concatenate([tiles, pad])
+
+
+def gather_tiles(local, rank: int, world: int, dist, dst: int = 0):
+    """Gather equally-sized per-rank tile buffers to `dst` (RCCL gather over xGMI on
+    GPUs, gloo on CPU).  Returns the list of buffers on dst, None elsewhere."""
+    if world == 1:
+        return [local]
+    if rank == dst:
+        bufs = [local.new_empty(local.shape) for _ in range(world)]
+        dist.gather(local, gather_list=bufs, dst=dst)
+        return bufs
+    dist.gather(local, dst=dst)
+    return None
