@@ -215,6 +215,9 @@ def main():
             "samples_per_s": round(samples / max_t, 1),
             "reference_queries_per_s": round(queries / max_t, 1),
             "kernel_ms": round(kern_ms, 3),
+            "per_launch": {"traced_rays": int(mine[1]), "node_visits": int(mine[4]), "tri_tests": int(mine[5]),
+                           "algorithmic_bytes": int(bytes_launch),
+                           "bytes_per_unit": {"node": NODE_BYTES, "tri": TRI_BYTES, "shade_per_ray": SHADE_BYTES}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
             "cpu_baseline": base,
