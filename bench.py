@@ -168,6 +168,8 @@ def main():
 
     mine = np.array([elapsed, st["traced_rays"], st["queries"], st["samples"], st["node_visits"],
                      st["tri_tests"], kern_ms], np.float64)
+    simt = {"path_loop": st["loop_lane_iters"] / max(64 * st["loop_wave_iters"], 1),
+            "bvh_loop": st["trav_lane_steps"] / max(64 * st["trav_wave_steps"], 1)}
     if world > 1:
         tm = torch.tensor(mine, device=dev)
         allv = [torch.zeros_like(tm) for _ in range(world)]
@@ -215,6 +217,7 @@ def main():
             "samples_per_s": round(samples / max_t, 1),
             "reference_queries_per_s": round(queries / max_t, 1),
             "kernel_ms": round(kern_ms, 3),
+            "simt_utilisation": {k: round(v, 4) for k, v in simt.items()},
             "per_launch": {"traced_rays": int(mine[1]), "node_visits": int(mine[4]), "tri_tests": int(mine[5]),
                            "algorithmic_bytes": int(bytes_launch),
                            "bytes_per_unit": {"node": NODE_BYTES, "tri": TRI_BYTES, "shade_per_ray": SHADE_BYTES}},

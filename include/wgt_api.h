@@ -108,7 +108,9 @@ typedef struct {
   uint64_t node_visits;  /* BVH nodes fetched */
   uint64_t tri_tests;    /* Moller-Trumbore tests */
   uint64_t pixels;
-  uint64_t reserved;
+  /* SIMT efficiency: iterations of the per-lane path loop / BVH loop counted once
+   * per wave (wave_*) and once per active lane (lane_*); lane/(64*wave) = utilisation */
+  uint64_t loop_wave_iters, loop_lane_iters, trav_wave_steps, trav_lane_steps;
   float kernel_ms;       /* hipEvent time of the (uninstrumented) render launch */
   float pad[3];
 } wgt_stats;

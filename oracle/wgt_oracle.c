@@ -373,7 +373,8 @@ static void tri_box(const o_tri *t, float lo[3], float hi[3]) {
   }
 }
 
-/* Slab spec: inverse direction with |d| < 1e-30 replaced by copysign(1e-30, d). */
+/* Slab spec: inverse direction with |d| < 1e-30 replaced by
+ * copysign(1e-30, d); per plane t = fma(b, inv, -(o*inv)). */
 static inline void inv_dir(v3 d, float inv[3]) {
   float dd[3] = {d.x, d.y, d.z};
   for (int c = 0; c < 3; ++c) {
@@ -382,13 +383,13 @@ static inline void inv_dir(v3 d, float inv[3]) {
     inv[c] = 1.0f / x;
   }
 }
-static inline void slab(const float o[3], const float inv[3], const float lo[3],
+static inline void slab(const float ot[3], const float inv[3], const float lo[3],
                         const float hi[3], float *tnear, float *tfar) {
   float n = -INFINITY, f = INFINITY;
   int first = 1;
   for (int c = 0; c < 3; ++c) {
-    float t0 = (lo[c] - o[c]) * inv[c];
-    float t1 = (hi[c] - o[c]) * inv[c];
+    float t0 = fmaf(lo[c], inv[c], ot[c]);
+    float t1 = fmaf(hi[c], inv[c], ot[c]);
     float a = t0 < t1 ? t0 : t1;
     float b = t0 < t1 ? t1 : t0;
     if (first) { n = a; f = b; first = 0; }
@@ -417,13 +418,13 @@ static inline int mt_test(v3 o, v3 d, const o_tri *tr, float *tout) {
   return 1;
 }
 
-static inline void tri_candidate(const o_scene *s, int i, v3 o, v3 d, const float of[3],
+static inline void tri_candidate(const o_scene *s, int i, v3 o, v3 d, const float ot[3],
                                  const float inv[3], float *best_t, uint32_t *best_i) {
   float t;
   if (!mt_test(o, d, &s->tris[i], &t)) return;
   if (!(t < *best_t || (t == *best_t && (uint32_t)i < *best_i))) return;
   float n, f;
-  slab(of, inv, &s->tbox[6 * i], &s->tbox[6 * i + 3], &n, &f);
+  slab(ot, inv, &s->tbox[6 * i], &s->tbox[6 * i + 3], &n, &f);
   if (!(n <= t && t <= f)) return;
   *best_t = t;
   *best_i = (uint32_t)i;
@@ -434,11 +435,11 @@ static void tris_closest(const o_scene *s, v3 o, v3 d, int brute, float *bt, uin
   float best_t = kRayMax;
   uint32_t best_i = kNoHit;
   if (s->nT > 0) {
-    float of[3] = {o.x, o.y, o.z};
     float inv[3];
     inv_dir(d, inv);
+    float ot[3] = {-(o.x * inv[0]), -(o.y * inv[1]), -(o.z * inv[2])};
     if (brute) {
-      for (int i = 0; i < s->nT; ++i) tri_candidate(s, i, o, d, of, inv, &best_t, &best_i);
+      for (int i = 0; i < s->nT; ++i) tri_candidate(s, i, o, d, ot, inv, &best_t, &best_i);
     } else {
       int stack[128];
       int sp = 0;
@@ -446,11 +447,11 @@ static void tris_closest(const o_scene *s, v3 o, v3 d, int brute, float *bt, uin
       while (sp > 0) {
         const obvh_node *nd = &s->nodes[stack[--sp]];
         float n, f;
-        slab(of, inv, nd->lo, nd->hi, &n, &f);
+        slab(ot, inv, nd->lo, nd->hi, &n, &f);
         if (!(n <= f && n <= best_t && f >= kRayMin)) continue;
         if (nd->count > 0) {
           for (int k = 0; k < nd->count; ++k)
-            tri_candidate(s, s->tidx[nd->first + k], o, d, of, inv, &best_t, &best_i);
+            tri_candidate(s, s->tidx[nd->first + k], o, d, ot, inv, &best_t, &best_i);
         } else {
           stack[sp++] = nd->right;
           stack[sp++] = nd->left;

@@ -33,11 +33,13 @@ NO_HIT = 0xFFFFFFFF
 class WgtStats(ctypes.Structure):
     _fields_ = [("queries", ctypes.c_uint64), ("traced_rays", ctypes.c_uint64), ("samples", ctypes.c_uint64),
                 ("nan_rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64),
-                ("pixels", ctypes.c_uint64), ("reserved", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
+                ("pixels", ctypes.c_uint64), ("loop_wave_iters", ctypes.c_uint64),
+                ("loop_lane_iters", ctypes.c_uint64), ("trav_wave_steps", ctypes.c_uint64),
+                ("trav_lane_steps", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
                 ("pad", ctypes.c_float * 3)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k not in ("pad", "reserved")}
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
 
 
 class WgtSceneInfo(ctypes.Structure):

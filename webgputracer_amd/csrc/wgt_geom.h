@@ -46,21 +46,20 @@ WGT_HD float safe_inv(float x) {
   return 1.0f / x;
 }
 
-// Slab interval of box [lo, hi] for origin o and inverse direction inv.
-WGT_HD void slab(f3 o, f3 inv, f3 lo, f3 hi, float& tnear, float& tfar) {
-  float t0x = (lo.x - o.x) * inv.x, t1x = (hi.x - o.x) * inv.x;
-  float t0y = (lo.y - o.y) * inv.y, t1y = (hi.y - o.y) * inv.y;
-  float t0z = (lo.z - o.z) * inv.z, t1z = (hi.z - o.z) * inv.z;
-  float nx = t0x < t1x ? t0x : t1x, fx = t0x < t1x ? t1x : t0x;
-  float ny = t0y < t1y ? t0y : t1y, fy = t0y < t1y ? t1y : t0y;
-  float nz = t0z < t1z ? t0z : t1z, fz = t0z < t1z ? t1z : t0z;
-  float n = ny > nx ? ny : nx;
-  n = nz > n ? nz : n;
-  float f = fy < fx ? fy : fx;
-  f = fz < f ? fz : f;
-  tnear = n;
-  tfar = f;
+// Slab interval of box [lo, hi] for a ray given as inv = 1/d and ot = -(o * inv):
+// t = fma(b, inv, ot) per plane.  The formula is monotone in the plane coordinate
+// b (exact fma, monotone rounding), which is all the nesting argument needs.  No
+// operand is NaN (inv finite, boxes finite), so min/max need no NaN rules.
+WGT_HD void slab(f3 ot, f3 inv, f3 lo, f3 hi, float& tnear, float& tfar) {
+  const float t0x = __builtin_fmaf(lo.x, inv.x, ot.x), t1x = __builtin_fmaf(hi.x, inv.x, ot.x);
+  const float t0y = __builtin_fmaf(lo.y, inv.y, ot.y), t1y = __builtin_fmaf(hi.y, inv.y, ot.y);
+  const float t0z = __builtin_fmaf(lo.z, inv.z, ot.z), t1z = __builtin_fmaf(hi.z, inv.z, ot.z);
+  tnear = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                          __builtin_fminf(t0z, t1z));
+  tfar = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                         __builtin_fmaxf(t0z, t1z));
 }
+WGT_HD f3 slab_offset(f3 o, f3 inv) { return f3{-(o.x * inv.x), -(o.y * inv.y), -(o.z * inv.z)}; }
 
 // Two-sided Moller-Trumbore (fixed op order).
 WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {

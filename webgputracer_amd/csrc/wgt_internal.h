@@ -19,7 +19,7 @@
 namespace wgt {
 
 constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
-constexpr int kStackLds = 32;     // per-lane traversal stack entries in LDS
+constexpr int kStackLds = 24;     // per-lane traversal stack entries in LDS (6 KB/wave)
 constexpr int kStackScratch = 64; // overflow entries in private (scratch) memory
 constexpr int kMaxBvhDepth = kStackLds + kStackScratch - 2;
 
@@ -48,6 +48,11 @@ struct DevFrame {
   uint32_t sqrt_spp;
   uint32_t W, H;
   uint32_t tw, th, n_tiles;
+  // kernel selection and phase-split thresholds (k_render_ps): switch from the
+  // service to the traversal phase once >= ps_to_trav lanes traverse, and back
+  // once <= ps_to_service lanes still traverse.
+  uint32_t kernel;  // 0 = phase-split (scenes with triangles), 1 = simple
+  uint32_t ps_to_trav, ps_to_service;
 };
 
 enum {
@@ -58,7 +63,11 @@ enum {
   CNT_NODES,
   CNT_TRIS,
   CNT_PIXELS,
-  CNT_N = 8
+  CNT_LOOP_WAVE,
+  CNT_LOOP_LANE,
+  CNT_TRAV_WAVE,
+  CNT_TRAV_LANE,
+  CNT_N = 12
 };
 
 // Launchers implemented in wgt_kernels.hip

@@ -1,15 +1,25 @@
 // wgt_kernels.hip — the MI355X (gfx950) path-tracing kernels.
 //
-// k_render: one lane per pixel, one wave (64 lanes = 8x8 pixels) per block.  Each
-// lane runs its pixel's whole compute_sample (path_tracer.wgsl:374-398) as a flat
-// state machine — one closest-hit query + one shading step per loop iteration — so
-// the 64 lanes of a wave stay converged on the trace even when their paths are at
-// different samples/bounces.  The per-pixel RNG stream is serial across samples
-// (path_tracer.wgsl:378, 381-395), so there is no sample-level parallelism.
+// One lane per pixel, one wave (64 lanes = 8x8 pixels) per block.  Each lane runs
+// its pixel's whole compute_sample (path_tracer.wgsl:374-398); the per-pixel RNG
+// stream is serial across samples (path_tracer.wgsl:378, 381-395), so there is no
+// sample-level parallelism — parallelism is over pixels only.
 //
 // sample_hit (path_tracer.wgsl:290-310) = linear scan of lights and quads (scalar
-// loads: the scene is wave-uniform), BVH2 traversal over triangles (per-lane
-// LDS stack, Moller-Trumbore in fp32, wgt_geom.h), then the sphere scan.
+// loads: the scene is wave-uniform), BVH2 traversal over triangles (per-lane LDS
+// stack, Moller-Trumbore in fp32, wgt_geom.h), then the sphere scan.
+//
+// Two kernels compute bit-identical results:
+//  * k_render (simple): a flat per-lane loop, one closest-hit query + one shading
+//    step per iteration.  Used for scenes without triangles (the Cornell box).
+//  * k_render_ps (phase-split, scenes with triangles): the wave alternates a
+//    SERVICE phase (finalise the hit of lanes whose traversal ended, shade, start
+//    the next ray: camera ray or bounce, quad scan, root-node test) and a
+//    TRAVERSAL phase (one BVH node or leaf per lane per step).  A phase ends when
+//    too few lanes are left for it (wave-uniform ballot counts), so lanes whose
+//    ray left the BVH early pick up new rays while the long traversals continue:
+//    the traversal loop runs at 10 % SIMT utilisation in k_render on the bunny
+//    stand-in (profiles/r01_*), which this structure removes.
 //
 // NaN rays (any NaN in start/dir) are resolved without tracing: every rejection
 // test of the reference is false for NaN, so the last primitive of the scan — the
@@ -44,8 +54,23 @@ __device__ __forceinline__ void hit_init(Hit& h) {
   h.col = f3{0.0f, 0.0f, 0.0f};
 }
 
-// path_tracer.wgsl:314-338.  `qt` receives t of the accepted quad (used only as
-// a conservative bound for the triangle search).
+// Accept quad q at parameter t with distance ray_dist (tail of intersect_quad).
+__device__ __forceinline__ void quad_accept(f3 o, f3 d, const float4* __restrict__ q, uint32_t id,
+                                            float t, float ray_dist, Hit& h) {
+  const f3 qn = xyz(q[3]);
+  const bool ff = dot(d, qn) < 0.0f;
+  const float4 c = q[5];
+  h.dist = ray_dist;
+  h.prim = id;
+  h.emissive = c.w > 0.0f;
+  h.front_face = ff;
+  h.pos = o + t * d;
+  h.norm = ff ? qn : -qn;
+  h.col = xyz(c);
+}
+
+// path_tracer.wgsl:314-338.  `qt` receives t of the accepted quad: the triangle
+// search bound, and what finalize needs to rebuild the quad hit bit for bit.
 __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict__ q, uint32_t id,
                                            Hit& h, float& qt) {
   const f3 qn = xyz(q[3]);
@@ -62,15 +87,7 @@ __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict_
   const float a = dot(w, cross(hit_vec, xyz(q[2])));
   const float b = dot(w, cross(xyz(q[1]), hit_vec));
   if ((a < 0.0f) || (1.0f < a) || (b < 0.0f) || (1.0f < b)) return;
-  const bool ff = dot(d, qn) < 0.0f;
-  const float4 c = q[5];
-  h.dist = ray_dist;
-  h.prim = id;
-  h.emissive = c.w > 0.0f;
-  h.front_face = ff;
-  h.pos = pos;
-  h.norm = ff ? qn : -qn;
-  h.col = xyz(c);
+  quad_accept(o, d, q, id, t, ray_dist, h);
   qt = t;
 }
 
@@ -106,117 +123,229 @@ __device__ __forceinline__ void isect_sphere(f3 o, f3 d, const float4* __restric
   h.col = xyz(col);
 }
 
+__device__ __forceinline__ void quad_scan(const DevScene& sc, f3 o, f3 d, Hit& h, float& qt) {
+  hit_init(h);
+  qt = kRayMax;
+  const uint32_t nlq = sc.n_lights + sc.n_quads;
+  for (uint32_t k = 0; k < nlq; ++k) isect_quad(o, d, sc.quads + 6 * k, k, h, qt);
+}
+
+// The quad part of a hit rebuilt from (prim, t): the same operations as isect_quad.
+__device__ __forceinline__ void quad_rebuild(const DevScene& sc, f3 o, f3 d, uint32_t prim, float t,
+                                             Hit& h) {
+  hit_init(h);
+  if (prim == kNoHit) return;
+  const f3 pos = o + t * d;
+  quad_accept(o, d, sc.quads + 6 * prim, prim, t, distance(pos, o), h);
+}
+
+__device__ __forceinline__ uint32_t last_prim(const DevScene& sc) {
+  return sc.n_lights + sc.n_quads + sc.n_tris + sc.n_spheres - 1u;
+}
+
+// A NaN ray's hit: the last sphere (every rejection test is false for NaN).
+__device__ __forceinline__ void nan_hit(const DevScene& sc, f3 o, f3 d, Hit& h) {
+  hit_init(h);
+  const uint32_t k = sc.n_spheres - 1;
+  isect_sphere(o, d, sc.spheres + 2 * k, sc.n_lights + sc.n_quads + sc.n_tris + k, h);
+}
+
 struct TravStats {
-  uint32_t nodes, tris;
+  uint32_t nodes, tris, wave_steps, lane_steps;
 };
 
-// Closest triangle = min (t, index) with t < bound (or t <= bound and index < bi
-// when bi = kNoHit).  Per-lane stack: kStackLds entries in LDS (stride kBlock,
-// conflict-free), overflow in private memory.
+// Counts one per wave (first active lane) and one per active lane.
+__device__ __forceinline__ void simt_count(uint32_t& wave, uint32_t& lane) {
+  const unsigned long long b = __ballot(1);
+  if (__lane_id() == (unsigned)(__ffsll((long long)b) - 1)) ++wave;
+  ++lane;
+}
+
+// Resumable BVH2 traversal: closest triangle = min (t, index) with t < bound (or
+// t <= bound and index < bi when bi = kNoHit).  Per-lane stack: kStackLds entries
+// in LDS (stride kBlock, conflict-free), overflow in private (scratch) memory.
+struct Trav {
+  f3 inv, ot;
+  float bt;
+  uint32_t bi;
+  int ref;
+  int sp;
+  uint32_t iters;
+  bool found;
+};
+
+__device__ __forceinline__ void trav_init(f3 o, f3 d, bool quad_hit, float qt, Trav& t) {
+  t.inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
+  t.ot = slab_offset(o, t.inv);
+  // a triangle must satisfy t < t_quad to beat a quad hit (ray_dist is monotone in t)
+  t.bt = quad_hit ? qt : kRayMax;
+  t.bi = quad_hit ? 0u : kNoHit;
+  t.ref = 0;
+  t.sp = 0;
+  t.iters = 0;
+  t.found = false;
+}
+
+// One node or one leaf.  Returns true when the traversal has finished.
 template <bool STATS>
-__device__ __forceinline__ bool bvh_closest(const DevScene& sc, f3 o, f3 d, float& best_t,
-                                            uint32_t& best_i, int* __restrict__ lds,
-                                            TravStats& st) {
-  const f3 inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
-  int priv[kStackScratch];
-  int sp = 0;
-  int ref = 0;
-  bool found = false;
-  uint32_t iters = 0;
-  for (;;) {
-    if (ref >= 0) {
-      const float4* __restrict__ n = sc.nodes + 4 * ref;
-      const float4 a = n[0], b = n[1], c = n[2], e = n[3];
-      if (STATS) st.nodes++;
-      float n0, f0, n1, f1;
-      slab(o, inv, f3{a.x, a.z, c.x}, f3{a.y, a.w, c.y}, n0, f0);
-      slab(o, inv, f3{b.x, b.z, c.z}, f3{b.y, b.w, c.w}, n1, f1);
-      const bool h0 = (n0 <= f0) & (n0 <= best_t) & (f0 >= kRayMin);
-      const bool h1 = (n1 <= f1) & (n1 <= best_t) & (f1 >= kRayMin);
-      const int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-      if (h0 && h1) {
-        const bool swap = n1 < n0;
-        const int nearr = swap ? r1 : r0;
-        const int farr = swap ? r0 : r1;
-        if (sp < kStackLds) lds[sp * kBlock] = farr;
-        else if (sp < kStackLds + kStackScratch) priv[sp - kStackLds] = farr;
-        ++sp;
-        ref = nearr;
-        continue;
-      }
-      if (h0) { ref = r0; continue; }
-      if (h1) { ref = r1; continue; }
-    } else {
-      const uint32_t first = leaf_first(ref), cnt = leaf_count(ref);
-      for (uint32_t k = 0; k < cnt; ++k) {
-        const float4* __restrict__ tp = sc.tris + 3 * (first + k);
-        const float4 A = tp[0], B = tp[1], C = tp[2];
-        if (STATS) st.tris++;
-        const f3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
-        float t;
-        if (mt_test(o, d, v0, e1, e2, t)) {
-          const uint32_t idx = __float_as_uint(A.w);
-          if (t < best_t || (t == best_t && idx < best_i)) {
-            f3 lo, hi;
-            tri_box(v0, e1, e2, lo, hi);
-            float bn, bf;
-            slab(o, inv, lo, hi, bn, bf);
-            if (bn <= t && t <= bf) {
-              best_t = t;
-              best_i = idx;
-              found = true;
-            }
+__device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& t,
+                                          int* __restrict__ lds, int* priv, TravStats& st) {
+  if (STATS) simt_count(st.wave_steps, st.lane_steps);
+  if (t.ref >= 0) {
+    const float4* __restrict__ n = sc.nodes + 4 * t.ref;
+    const float4 a = n[0], b = n[1], c = n[2], e = n[3];
+    if (STATS) st.nodes++;
+    float n0, f0, n1, f1;
+    slab(t.ot, t.inv, f3{a.x, a.z, c.x}, f3{a.y, a.w, c.y}, n0, f0);
+    slab(t.ot, t.inv, f3{b.x, b.z, c.z}, f3{b.y, b.w, c.w}, n1, f1);
+    const bool h0 = (n0 <= f0) & (n0 <= t.bt) & (f0 >= kRayMin);
+    const bool h1 = (n1 <= f1) & (n1 <= t.bt) & (f1 >= kRayMin);
+    const int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
+    if (h0 && h1) {
+      const bool swap = n1 < n0;
+      const int nearr = swap ? r1 : r0;
+      const int farr = swap ? r0 : r1;
+      if (t.sp < kStackLds) lds[t.sp * kBlock] = farr;
+      else if (t.sp < kStackLds + kStackScratch) priv[t.sp - kStackLds] = farr;
+      ++t.sp;
+      t.ref = nearr;
+      return false;
+    }
+    if (h0) { t.ref = r0; return false; }
+    if (h1) { t.ref = r1; return false; }
+  } else {
+    const uint32_t first = leaf_first(t.ref), cnt = leaf_count(t.ref);
+    for (uint32_t k = 0; k < cnt; ++k) {
+      const float4* __restrict__ tp = sc.tris + 3 * (first + k);
+      const float4 A = tp[0], B = tp[1], C = tp[2];
+      if (STATS) st.tris++;
+      const f3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
+      float tt;
+      if (mt_test(o, d, v0, e1, e2, tt)) {
+        const uint32_t idx = __float_as_uint(A.w);
+        if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
+          f3 lo, hi;
+          tri_box(v0, e1, e2, lo, hi);
+          float bn, bf;
+          slab(t.ot, t.inv, lo, hi, bn, bf);
+          if (bn <= tt && tt <= bf) {
+            t.bt = tt;
+            t.bi = idx;
+            t.found = true;
           }
         }
       }
     }
-    if (sp == 0 || ++iters > sc.max_iters) break;
-    --sp;
-    ref = sp < kStackLds ? lds[sp * kBlock] : priv[sp - kStackLds];
   }
-  return found;
+  if (t.sp == 0 || ++t.iters > sc.max_iters) return true;
+  --t.sp;
+  // pop: the LDS read is unconditional (ds_read); scratch only on overflow
+  int v = lds[(t.sp < kStackLds ? t.sp : kStackLds - 1) * kBlock];
+  if (t.sp >= kStackLds) v = priv[t.sp - kStackLds];
+  t.ref = v;
+  return false;
 }
 
-// sample_hit (path_tracer.wgsl:290-310) + triangles between quads and spheres.
-template <bool TRIS, bool STATS>
-__device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* __restrict__ lds,
-                                           Hit& h, TravStats& st) {
-  hit_init(h);
+// Merge the triangle result into the quad hit, then scan the spheres: the end of
+// sample_hit (path_tracer.wgsl:305-309) with triangles between quads and spheres.
+__device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const Trav& t, Hit& h) {
   const uint32_t nlq = sc.n_lights + sc.n_quads;
-  if (has_nan(o) || has_nan(d)) {
-    // every rejection is false for NaN: the last primitive scanned wins
-    const uint32_t k = sc.n_spheres - 1;
-    isect_sphere(o, d, sc.spheres + 2 * k, nlq + sc.n_tris + k, h);
-    return;
-  }
-  float qt = kRayMax;
-  for (uint32_t k = 0; k < nlq; ++k) isect_quad(o, d, sc.quads + 6 * k, k, h, qt);
-  if (TRIS) {
-    float bt = kRayMax;
-    uint32_t bi = kNoHit;
-    if (h.prim != kNoHit) {  // a triangle must satisfy t < t_quad to win (ray_dist is monotone in t)
-      bt = qt;
-      bi = 0u;
-    }
-    if (bvh_closest<STATS>(sc, o, d, bt, bi, lds, st)) {
-      const f3 pos = o + bt * d;
-      const float ray_dist = distance(pos, o);
-      if (!(ray_dist >= h.dist)) {
-        const float4 s0 = sc.tshade[2 * bi], s1 = sc.tshade[2 * bi + 1];
-        const f3 fn = xyz(s0);
-        const bool ff = dot(d, fn) < 0.0f;
-        h.dist = ray_dist;
-        h.prim = nlq + bi;
-        h.emissive = s0.w > 0.0f;
-        h.front_face = ff;
-        h.pos = pos;
-        h.norm = ff ? fn : -fn;
-        h.col = xyz(s1);
-      }
+  if (t.found) {
+    const f3 pos = o + t.bt * d;
+    const float ray_dist = distance(pos, o);
+    if (!(ray_dist >= h.dist)) {
+      const float4 s0 = sc.tshade[2 * t.bi], s1 = sc.tshade[2 * t.bi + 1];
+      const f3 fn = xyz(s0);
+      const bool ff = dot(d, fn) < 0.0f;
+      h.dist = ray_dist;
+      h.prim = nlq + t.bi;
+      h.emissive = s0.w > 0.0f;
+      h.front_face = ff;
+      h.pos = pos;
+      h.norm = ff ? fn : -fn;
+      h.col = xyz(s1);
     }
   }
   for (uint32_t k = 0; k < sc.n_spheres; ++k)
     isect_sphere(o, d, sc.spheres + 2 * k, nlq + sc.n_tris + k, h);
+}
+
+// Full sample_hit for one ray (k_trace, k_render).
+template <bool TRIS, bool STATS>
+__device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* __restrict__ lds,
+                                           int* priv, Hit& h, TravStats& st) {
+  if (has_nan(o) || has_nan(d)) {
+    nan_hit(sc, o, d, h);
+    return;
+  }
+  float qt;
+  quad_scan(sc, o, d, h, qt);
+  Trav t;
+  trav_init(o, d, h.prim != kNoHit, qt, t);
+  if (TRIS) {
+    while (!trav_step<STATS>(sc, o, d, t, lds, priv, st)) {
+    }
+  }
+  finish_hit(sc, o, d, t, h);
+}
+
+struct Light {
+  f3 pos, right, up;
+};
+
+// raytrace() after sample_hit (path_tracer.wgsl:267-287).  Returns path.end.
+__device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const Hit& h, int depth,
+                                      uint32_t& seed, f3& ro, f3& rd, f3& pc) {
+  if (h.emissive) {
+    if (depth != 0) {
+      const float ff = h.front_face ? 1.0f : 0.0f;
+      pc = (ff * h.col) * pc;
+    } else {
+      pc = h.col;
+    }
+    return true;
+  }
+  // sample_direction (path_tracer.wgsl:146-154)
+  const f3 w = normalize(h.norm);  // onb.w of build_onb_from_w(hit.norm)
+  f3 sdir;
+  if (rand_next(seed) > 0.5f) {
+    // sample_from_cosine: build_onb_from_w (:133-140) + rand_cos_dir (:123-131)
+    const f3 a = (sign_w(w.x) * w.x) > 0.9f ? f3{0.0f, 1.0f, 0.0f} : f3{1.0f, 0.0f, 0.0f};
+    const f3 v = normalize(cross(w, a));
+    const f3 u = cross(w, v);
+    const float r1 = rand_next(seed);
+    const float r2 = rand_next(seed);
+    const float z = __builtin_sqrtf(1.0f - r2);
+    const float phi = 2.0f * kPI * r1;
+    float sphi, cphi;
+    sincos_w(phi, sphi, cphi);
+    const float sr2 = __builtin_sqrtf(r2);
+    const float lx2 = cphi * sr2;
+    const float ly2 = sphi * sr2;
+    sdir = (lx2 * u + ly2 * v) + z * w;
+  } else {
+    // sample_from_light (:163-168), not normalised
+    const float r1 = rand_next(seed);
+    const float r2 = rand_next(seed);
+    sdir = ((L.pos + r1 * L.right) + r2 * L.up) - h.pos;
+  }
+  // mixture_pdf (:191-193) = 0.5*cosine_pdf + 0.5*light_area_pdf
+  const float len = length(sdir);
+  const f3 nd = sdir / len;  // normalize(dir): shared by cosine_pdf, the light cosine and :282
+  const float cs = dot(nd, w);
+  const float cpdf = cs <= 0.0f ? 0.0f : cs * k_1_PI;
+  const float dist2 = len * len;
+  const float light_cosine = fabs_w(nd.y) + kRayMin;
+  const float lpdf = dist2 / (light_cosine * sc.light_area);
+  const float pdf_val = 0.5f * cpdf + 0.5f * lpdf;
+  // scattering_pdf (:217-220) normalises the already normalised direction again
+  const f3 nd2 = normalize(nd);
+  const float cs2 = dot(h.norm, nd2);
+  const float spdf = cs2 < 0.0f ? 0.0f : cs2 * k_1_PI;
+  pc = (spdf * (pc * h.col)) / pdf_val;
+  ro = h.pos;
+  rd = nd;
+  return false;
 }
 
 __device__ __forceinline__ uint8_t unorm8(float x) {
@@ -225,151 +354,248 @@ __device__ __forceinline__ uint8_t unorm8(float x) {
   return (uint8_t)__builtin_floorf(c * 255.0f + 0.5f);
 }
 
+// Per-pixel state shared by both kernels.
+struct Pixel {
+  uint32_t x, y;
+  uint32_t seed;
+  uint32_t k, si, sj;  // sample index and its (s_i, s_j)
+  f3 col;
+  uint32_t hit0;
+};
+
+struct Counters {
+  uint32_t q, tr, nan, lw, ll;
+};
+
+// Pixel of this lane, or false if the lane has none.
+__device__ __forceinline__ bool pixel_setup(const DevFrame& fr, const wgt_tile* __restrict__ tiles,
+                                            uint32_t& tile, uint32_t& lx, uint32_t& ly, Pixel& px) {
+  const uint32_t bx = (fr.tw + 7u) >> 3, by = (fr.th + 7u) >> 3;
+  const uint32_t bpt = bx * by;
+  tile = blockIdx.x / bpt;
+  const uint32_t rem = blockIdx.x - tile * bpt;
+  lx = (rem % bx) * 8u + (threadIdx.x & 7u);
+  ly = (rem / bx) * 8u + (threadIdx.x >> 3);
+  if (tile >= fr.n_tiles || lx >= fr.tw || ly >= fr.th) return false;
+  const wgt_tile td = tiles[tile];
+  px.x = td.x0 + lx;
+  px.y = td.y0 + ly;
+  if (px.x >= fr.W || px.y >= fr.H) return false;  // path_tracer.wgsl:377
+  px.seed = px.x + px.y * fr.W + td.seed * fr.W * fr.H;  // path_tracer.wgsl:378
+  px.k = px.si = px.sj = 0;
+  px.col = f3{0.0f, 0.0f, 0.0f};
+  px.hit0 = kNoHit;
+  return true;
+}
+
+// setup_camera_ray + pixel_sample_square (path_tracer.wgsl:232-262) for sample px.k
+__device__ __forceinline__ void camera_ray(const DevFrame& fr, Pixel& px, f3& ro, f3& rd) {
+  const f3 origin = f3{fr.ox, fr.oy, fr.oz};
+  const f3 du = f3{fr.dux, fr.duy, fr.duz};
+  const f3 dv = f3{fr.dvx, fr.dvy, fr.dvz};
+  const f3 pixel_center = (f3{fr.pox, fr.poy, fr.poz} + (float)px.x * du) + (float)px.y * dv;
+  const float sx = -0.5f + fr.recip_sqrt_spp * ((float)px.si + rand_next(px.seed));
+  const float sy = -0.5f + fr.recip_sqrt_spp * ((float)px.sj + rand_next(px.seed));
+  const f3 pixel_sample = pixel_center + (sx * du + sy * dv);
+  ro = origin;
+  rd = pixel_sample - origin;
+}
+
+// col += max(path.col, 0) / f32(spp) (path_tracer.wgsl:393) and advance to the next sample
+__device__ __forceinline__ void end_sample(const DevFrame& fr, Pixel& px, f3 pc) {
+  px.col = px.col + f3{max0(pc.x) / fr.fspp, max0(pc.y) / fr.fspp, max0(pc.z) / fr.fspp};
+  ++px.k;
+  if (++px.si == fr.sqrt_spp) { px.si = 0; ++px.sj; }
+}
+
+// NaN-absorbed for the rest of the path: 3 rand() per remaining bounce, colour NaN.
+template <bool STATS>
+__device__ __forceinline__ void skip_nan_path(const DevScene& sc, const DevFrame& fr, Pixel& px,
+                                              int depth, Counters& c) {
+  px.seed = lcg_jump(px.seed, 3u * (uint32_t)(kRayDepth - depth));
+  if (STATS) {
+    c.q += (uint32_t)(kRayDepth - depth);
+    c.nan += (uint32_t)(kRayDepth - depth);
+  }
+  if (px.k == 0 && depth == 0) px.hit0 = last_prim(sc);
+  // col += max(NaN, 0) / spp == col + 0
+  ++px.k;
+  if (++px.si == fr.sqrt_spp) { px.si = 0; ++px.sj; }
+}
+
+__device__ __forceinline__ void write_pixel(const DevFrame& fr, uint32_t tile, uint32_t lx,
+                                            uint32_t ly, const Pixel& px, uchar4* out8, float4* out32,
+                                            uint32_t* outhit) {
+  const size_t o = ((size_t)tile * fr.th + ly) * fr.tw + lx;
+  if (out32) out32[o] = make_float4(px.col.x, px.col.y, px.col.z, 1.0f);
+  if (out8) out8[o] = make_uchar4(unorm8(px.col.x), unorm8(px.col.y), unorm8(px.col.z), 255);
+  if (outhit) outhit[o] = px.hit0;
+}
+
+__device__ __forceinline__ void flush_counters(unsigned long long* __restrict__ counters,
+                                               const Counters& c, const TravStats& st,
+                                               uint32_t nsamp) {
+  atomicAdd(&counters[CNT_QUERIES], (unsigned long long)c.q);
+  atomicAdd(&counters[CNT_TRACED], (unsigned long long)c.tr);
+  atomicAdd(&counters[CNT_SAMPLES], (unsigned long long)nsamp);
+  atomicAdd(&counters[CNT_NAN], (unsigned long long)c.nan);
+  atomicAdd(&counters[CNT_NODES], (unsigned long long)st.nodes);
+  atomicAdd(&counters[CNT_TRIS], (unsigned long long)st.tris);
+  atomicAdd(&counters[CNT_PIXELS], 1ull);
+  atomicAdd(&counters[CNT_LOOP_WAVE], (unsigned long long)c.lw);
+  atomicAdd(&counters[CNT_LOOP_LANE], (unsigned long long)c.ll);
+  atomicAdd(&counters[CNT_TRAV_WAVE], (unsigned long long)st.wave_steps);
+  atomicAdd(&counters[CNT_TRAV_LANE], (unsigned long long)st.lane_steps);
+}
+
 template <bool TRIS, bool STATS>
 __global__ void __launch_bounds__(kBlock)
 k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
          float4* __restrict__ out32, uint32_t* __restrict__ outhit,
          unsigned long long* __restrict__ counters) {
   __shared__ int s_stack[kStackLds * kBlock];
-  const uint32_t bx = (fr.tw + 7u) >> 3, by = (fr.th + 7u) >> 3;
-  const uint32_t bpt = bx * by;
-  const uint32_t tile = blockIdx.x / bpt;
-  const uint32_t rem = blockIdx.x - tile * bpt;
-  const uint32_t lx = (rem % bx) * 8u + (threadIdx.x & 7u);
-  const uint32_t ly = (rem / bx) * 8u + (threadIdx.x >> 3);
-  if (tile >= fr.n_tiles || lx >= fr.tw || ly >= fr.th) return;
-  const wgt_tile td = tiles[tile];
-  const uint32_t x = td.x0 + lx, y = td.y0 + ly;
-  if (x >= fr.W || y >= fr.H) return;  // path_tracer.wgsl:377
+  uint32_t tile, lx, ly;
+  Pixel px;
+  if (!pixel_setup(fr, tiles, tile, lx, ly, px)) return;
   int* lds = s_stack + threadIdx.x;
-
-  // path_tracer.wgsl:378
-  uint32_t seed = x + y * fr.W + td.seed * fr.W * fr.H;
-  const f3 origin = f3{fr.ox, fr.oy, fr.oz};
-  const f3 du = f3{fr.dux, fr.duy, fr.duz};
-  const f3 dv = f3{fr.dvx, fr.dvy, fr.dvz};
-  // pixel_center (path_tracer.wgsl:258), frame-invariant per pixel
-  const f3 pixel_center = (f3{fr.pox, fr.poy, fr.poz} + (float)x * du) + (float)y * dv;
-  const float4 L0 = sc.quads[0], L1 = sc.quads[1], L2 = sc.quads[2];
-  const f3 lpos = xyz(L0), lright = xyz(L1), lup = xyz(L2);
-
-  f3 col = f3{0.0f, 0.0f, 0.0f};
-  f3 ro = origin, rd = origin, pc = f3{1.0f, 1.0f, 1.0f};
+  int priv[kStackScratch];
+  const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
   const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
-  uint32_t k = 0, si = 0, sj = 0;
+  f3 ro{}, rd{}, pc{};
   int depth = 0;
-  uint32_t hit0 = kNoHit;
-  TravStats st{0u, 0u};
-  uint32_t c_q = 0, c_tr = 0, c_nan = 0;
+  TravStats st{0u, 0u, 0u, 0u};
+  Counters c{0u, 0u, 0u, 0u, 0u};
 
-  while (k < nsamp) {
+  while (px.k < nsamp) {
+    if (STATS) simt_count(c.lw, c.ll);
     if (depth == 0) {
-      // setup_camera_ray + pixel_sample_square (path_tracer.wgsl:232-262)
-      const float px = -0.5f + fr.recip_sqrt_spp * ((float)si + rand_next(seed));
-      const float py = -0.5f + fr.recip_sqrt_spp * ((float)sj + rand_next(seed));
-      const f3 pixel_sample = pixel_center + (px * du + py * dv);
-      ro = origin;
-      rd = pixel_sample - origin;
+      camera_ray(fr, px, ro, rd);
       pc = f3{1.0f, 1.0f, 1.0f};
     }
-    Hit h;
     const bool nanray = has_nan(ro) || has_nan(rd);
     if (nanray && !sc.last_sphere_emissive) {
-      // NaN-absorbed for the rest of the path: 3 rand() per remaining bounce.
-      seed = lcg_jump(seed, 3u * (uint32_t)(kRayDepth - depth));
-      if (STATS) {
-        c_q += (uint32_t)(kRayDepth - depth);
-        c_nan += (uint32_t)(kRayDepth - depth);
-      }
-      if (k == 0 && depth == 0) hit0 = sc.n_lights + sc.n_quads + sc.n_tris + sc.n_spheres - 1u;
-      // col += max(NaN, 0) / spp == col + 0
+      skip_nan_path<STATS>(sc, fr, px, depth, c);
       depth = 0;
-      ++k;
-      if (++si == fr.sqrt_spp) { si = 0; ++sj; }
       continue;
     }
-    sample_hit<TRIS, STATS>(sc, ro, rd, lds, h, st);
+    Hit h;
+    sample_hit<TRIS, STATS>(sc, ro, rd, lds, priv, h, st);
     if (STATS) {
-      ++c_q;
-      if (nanray) ++c_nan; else ++c_tr;
+      ++c.q;
+      if (nanray) ++c.nan; else ++c.tr;
     }
-    if (k == 0 && depth == 0) hit0 = h.prim;
-
-    // raytrace (path_tracer.wgsl:264-288)
-    bool end;
-    if (h.emissive) {
-      end = true;
-      if (depth != 0) {
-        const float ff = h.front_face ? 1.0f : 0.0f;
-        pc = (ff * h.col) * pc;
-      } else {
-        pc = h.col;
-      }
-    } else {
-      end = false;
-      // sample_direction (path_tracer.wgsl:146-154)
-      const f3 w = normalize(h.norm);  // onb.w of build_onb_from_w(hit.norm)
-      f3 sdir;
-      if (rand_next(seed) > 0.5f) {
-        // sample_from_cosine: build_onb_from_w (:133-140) + rand_cos_dir (:123-131)
-        const f3 a = (sign_w(w.x) * w.x) > 0.9f ? f3{0.0f, 1.0f, 0.0f} : f3{1.0f, 0.0f, 0.0f};
-        const f3 v = normalize(cross(w, a));
-        const f3 u = cross(w, v);
-        const float r1 = rand_next(seed);
-        const float r2 = rand_next(seed);
-        const float z = __builtin_sqrtf(1.0f - r2);
-        const float phi = 2.0f * kPI * r1;
-        float sphi, cphi;
-        sincos_w(phi, sphi, cphi);
-        const float sr2 = __builtin_sqrtf(r2);
-        const float lx2 = cphi * sr2;
-        const float ly2 = sphi * sr2;
-        sdir = (lx2 * u + ly2 * v) + z * w;
-      } else {
-        // sample_from_light (:163-168), not normalised
-        const float r1 = rand_next(seed);
-        const float r2 = rand_next(seed);
-        sdir = ((lpos + r1 * lright) + r2 * lup) - h.pos;
-      }
-      // mixture_pdf (:191-193) = 0.5*cosine_pdf + 0.5*light_area_pdf
-      const float len = length(sdir);
-      const f3 nd = sdir / len;  // normalize(dir): shared by cosine_pdf, the light cosine and :282
-      const float cs = dot(nd, w);
-      const float cpdf = cs <= 0.0f ? 0.0f : cs * k_1_PI;
-      const float dist2 = len * len;
-      const float light_cosine = fabs_w(nd.y) + kRayMin;
-      const float lpdf = dist2 / (light_cosine * sc.light_area);
-      const float pdf_val = 0.5f * cpdf + 0.5f * lpdf;
-      // scattering_pdf (:217-220) normalises the already normalised direction again
-      const f3 nd2 = normalize(nd);
-      const float cs2 = dot(h.norm, nd2);
-      const float spdf = cs2 < 0.0f ? 0.0f : cs2 * k_1_PI;
-      pc = (spdf * (pc * h.col)) / pdf_val;
-      ro = h.pos;
-      rd = nd;
-    }
+    if (px.k == 0 && depth == 0) px.hit0 = h.prim;
+    const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
     ++depth;
     if (end || depth == kRayDepth) {
-      col = col + f3{max0(pc.x) / fr.fspp, max0(pc.y) / fr.fspp, max0(pc.z) / fr.fspp};
+      end_sample(fr, px, pc);
       depth = 0;
-      ++k;
-      if (++si == fr.sqrt_spp) { si = 0; ++sj; }
     }
   }
+  write_pixel(fr, tile, lx, ly, px, out8, out32, outhit);
+  if (STATS) flush_counters(counters, c, st, nsamp);
+}
 
-  const size_t o = ((size_t)tile * fr.th + ly) * fr.tw + lx;
-  if (out32) out32[o] = make_float4(col.x, col.y, col.z, 1.0f);
-  if (out8) out8[o] = make_uchar4(unorm8(col.x), unorm8(col.y), unorm8(col.z), 255);
-  if (outhit) outhit[o] = hit0;
-  if (STATS) {
-    atomicAdd(&counters[CNT_QUERIES], (unsigned long long)c_q);
-    atomicAdd(&counters[CNT_TRACED], (unsigned long long)c_tr);
-    atomicAdd(&counters[CNT_SAMPLES], (unsigned long long)nsamp);
-    atomicAdd(&counters[CNT_NAN], (unsigned long long)c_nan);
-    atomicAdd(&counters[CNT_NODES], (unsigned long long)st.nodes);
-    atomicAdd(&counters[CNT_TRIS], (unsigned long long)st.tris);
-    atomicAdd(&counters[CNT_PIXELS], 1ull);
+// Phase-split kernel for scenes with triangles (see the file comment).
+template <bool STATS>
+__global__ void __launch_bounds__(kBlock)
+k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
+            float4* __restrict__ out32, uint32_t* __restrict__ outhit,
+            unsigned long long* __restrict__ counters) {
+  __shared__ int s_stack[kStackLds * kBlock];
+  uint32_t tile, lx, ly;
+  Pixel px;
+  if (!pixel_setup(fr, tiles, tile, lx, ly, px)) return;
+  int* lds = s_stack + threadIdx.x;
+  int priv[kStackScratch];
+  const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
+  const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
+  f3 ro{}, rd{}, pc{};
+  int depth = 0;
+  TravStats st{0u, 0u, 0u, 0u};
+  Counters c{0u, 0u, 0u, 0u, 0u};
+  Trav t;
+  uint32_t q_prim = kNoHit;  // quad part of the pending hit, rebuilt at finalisation
+  float q_t = kRayMax;
+  bool done = nsamp == 0, trav = false, pending = false;
+
+  for (;;) {
+    // ------------------------------------------------------------ service phase
+    for (;;) {
+      const bool need = !trav && !done;
+      if (!__any(need)) break;
+      if (need) {
+        if (STATS) simt_count(c.lw, c.ll);
+        if (pending) {
+          // finalise: rebuild the quad hit, merge triangles, scan spheres, shade
+          Hit h;
+          quad_rebuild(sc, ro, rd, q_prim, q_t, h);
+          finish_hit(sc, ro, rd, t, h);
+          if (STATS) { ++c.q; ++c.tr; }
+          if (px.k == 0 && depth == 0) px.hit0 = h.prim;
+          const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
+          ++depth;
+          if (end || depth == kRayDepth) {
+            end_sample(fr, px, pc);
+            depth = 0;
+          }
+          pending = false;
+        }
+        // start the next ray of this pixel
+        for (;;) {
+          if (px.k >= nsamp) {
+            done = true;
+            break;
+          }
+          if (depth == 0) {
+            camera_ray(fr, px, ro, rd);
+            pc = f3{1.0f, 1.0f, 1.0f};
+          }
+          if (has_nan(ro) || has_nan(rd)) {
+            if (!sc.last_sphere_emissive) {
+              skip_nan_path<STATS>(sc, fr, px, depth, c);
+              depth = 0;
+              continue;
+            }
+            Hit h;  // emissive last sphere: resolve the NaN ray here (no traversal)
+            nan_hit(sc, ro, rd, h);
+            if (STATS) { ++c.q; ++c.nan; }
+            if (px.k == 0 && depth == 0) px.hit0 = h.prim;
+            const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
+            ++depth;
+            if (end || depth == kRayDepth) {
+              end_sample(fr, px, pc);
+              depth = 0;
+            }
+            continue;
+          }
+          Hit h;
+          quad_scan(sc, ro, rd, h, q_t);
+          q_prim = h.prim;
+          trav_init(ro, rd, q_prim != kNoHit, q_t, t);
+          // the root node is tested here: rays that miss both root children never
+          // enter the traversal phase
+          if (trav_step<STATS>(sc, ro, rd, t, lds, priv, st)) pending = true;
+          else trav = true;
+          break;
+        }
+      }
+      if ((uint32_t)__popcll(__ballot(trav)) >= fr.ps_to_trav) break;
+    }
+    if (!__any(!done)) break;
+    // --------------------------------------------------------- traversal phase
+    for (;;) {
+      if (trav && trav_step<STATS>(sc, ro, rd, t, lds, priv, st)) {
+        trav = false;
+        pending = true;
+      }
+      const uint32_t ntrav = (uint32_t)__popcll(__ballot(trav));
+      if (ntrav == 0) break;
+      if (ntrav <= fr.ps_to_service && __any(!trav && !done)) break;
+    }
   }
+  write_pixel(fr, tile, lx, ly, px, out8, out32, outhit);
+  if (STATS) flush_counters(counters, c, st, nsamp);
 }
 
 template <bool TRIS>
@@ -379,11 +605,12 @@ k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __res
   __shared__ int s_stack[kStackLds * kBlock];
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
+  int priv[kStackScratch];
   const f3 o = f3{rays[i], rays[(size_t)n + i], rays[2 * (size_t)n + i]};
   const f3 d = f3{rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]};
   Hit h;
-  TravStats st{0u, 0u};
-  sample_hit<TRIS, false>(sc, o, d, s_stack + threadIdx.x, h, st);
+  TravStats st{0u, 0u, 0u, 0u};
+  sample_hit<TRIS, false>(sc, o, d, s_stack + threadIdx.x, priv, h, st);
   prim[i] = h.prim;
   dist[i] = h.dist;
 }
@@ -397,11 +624,14 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
   const dim3 grid((uint32_t)blocks), block(kBlock);
   const bool tris = sc.n_tris > 0;
+  const bool ps = tris && fr.kernel != 1;
   if (counters) {
-    if (tris) k_render<true, true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
+    if (ps) k_render_ps<true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
+    else if (tris) k_render<true, true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
     else k_render<false, true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
   } else {
-    if (tris) k_render<true, false><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
+    if (ps) k_render_ps<false><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
+    else if (tris) k_render<true, false><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
     else k_render<false, false><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
   }
   return hipGetLastError();

@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -83,6 +84,13 @@ void free_buf(DevBuf& b) {
 
 size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// Tuning knobs (read per launch; defaults are the measured best).
+uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* v = std::getenv(name);
+  if (!v || !*v) return dflt;
+  return (uint32_t)std::strtoul(v, nullptr, 10);
+}
+
 // setup_camera_ray's frame-invariant terms (path_tracer.wgsl:239-257), same fp32
 // operations as the WGSL per-invocation evaluation.
 DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
@@ -112,6 +120,9 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.sqrt_spp = (uint32_t)__builtin_sqrtf((float)cam.spp);
   fr.W = W;
   fr.H = H;
+  fr.kernel = env_u32("WGT_KERNEL", 0);
+  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 32);
+  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 16);
   return fr;
 }
 
@@ -135,6 +146,10 @@ void fill_stats(const unsigned long long* c, wgt_stats* s) {
   s->node_visits = c[CNT_NODES];
   s->tri_tests = c[CNT_TRIS];
   s->pixels = c[CNT_PIXELS];
+  s->loop_wave_iters = c[CNT_LOOP_WAVE];
+  s->loop_lane_iters = c[CNT_LOOP_LANE];
+  s->trav_wave_steps = c[CNT_TRAV_WAVE];
+  s->trav_lane_steps = c[CNT_TRAV_LANE];
 }
 
 }  // namespace
