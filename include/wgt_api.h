@@ -111,8 +111,12 @@ typedef struct {
   /* SIMT efficiency: iterations of the per-lane path loop / BVH loop counted once
    * per wave (wave_*) and once per active lane (lane_*); lane/(64*wave) = utilisation */
   uint64_t loop_wave_iters, loop_lane_iters, trav_wave_steps, trav_lane_steps;
-  float kernel_ms;       /* hipEvent time of the (uninstrumented) render launch */
-  float pad[3];
+  /* phase-split kernel: wave cycles (s_memtime) in the service / traversal phase */
+  uint64_t cyc_service, cyc_trav;
+  float kernel_ms;       /* hipEvent time of the (uninstrumented) render launches of the frame */
+  float trace_ms;        /* ... of which BVH-traversal kernel launches (wavefront) */
+  float shade_ms;        /* ... of which shading kernel launches (wavefront) */
+  uint32_t iterations;   /* wavefront bounce iterations (1 for a megakernel launch) */
 } wgt_stats;
 
 typedef struct {
@@ -152,12 +156,19 @@ int wgt_render_tile(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint3
                     uint32_t x0, uint32_t y0, uint32_t tw, uint32_t th, uint8_t *rgba8_out,
                     float *rgba32f_out, uint32_t *hit_id_out, wgt_stats *stats);
 
-/* Asynchronous tile-list launch with DEVICE buffers: n_tiles tiles of tw x th
- * (d_tiles: device array of wgt_tile) written compactly, tile after tile
- * (out[(t*th + ly)*tw + lx]).  cam->seed is ignored (per-tile seeds). */
+/* Tile-list launch with DEVICE buffers: n_tiles tiles of tw x th (d_tiles: device
+ * array of wgt_tile) written compactly, tile after tile (out[(t*th + ly)*tw + lx]).
+ * cam->seed is ignored (per-tile seeds).  Asynchronous for megakernel scenes; for
+ * scenes with triangles the wavefront loop polls a device completion counter, so
+ * the call returns when the frame is done (work is ordered on `stream`). */
 int wgt_render_tiles_async(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint32_t H,
                            uint32_t tw, uint32_t th, const wgt_tile *d_tiles, uint32_t n_tiles,
                            void *d_rgba8, float *d_rgba32f, uint32_t *d_hit_id, void *stream);
+/* Timing pass for the same launch: uninstrumented kernels with a hipEvent pair per
+ * launch; fills kernel_ms / trace_ms / shade_ms / iterations (synchronous). */
+int wgt_render_tiles_profile(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint32_t H,
+                             uint32_t tw, uint32_t th, const wgt_tile *d_tiles, uint32_t n_tiles,
+                             wgt_stats *stats);
 /* Counting pass for the same launch (instrumented kernel; synchronous). */
 int wgt_render_tiles_stats(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint32_t H,
                            uint32_t tw, uint32_t th, const wgt_tile *d_tiles, uint32_t n_tiles,

@@ -236,3 +236,19 @@ def test_sponza_render_parity(ctx, wgt, oracle):
     check_counters(g["stats"], r["counters"], oracle)
     info = ctx.scene_info()
     assert info["n_tris"] == len(T) and info["bvh_max_depth"] <= 94
+
+
+@pytest.mark.parametrize("kernel", ["0", "1", "2"])
+def test_kernel_families_agree_with_oracle(ctx, wgt, oracle, bunny, kernel, monkeypatch):
+    """wavefront (0), simple megakernel (1) and phase-split megakernel (2) are all
+    bit-exact against the oracle (the tuning knobs change speed only)."""
+    (L, Q, S, T), osc = bunny
+    monkeypatch.setenv("WGT_KERNEL", kernel)
+    monkeypatch.setenv("WGT_WF_RAYS", "2")
+    monkeypatch.setenv("WGT_WF_CHUNK", "256")
+    ctx.upload_scene(L, Q, S, T)
+    g = ctx.render_tile(wgt.camera_param(16 / 9, 4, 21), 72, 40, stats=True)
+    r = osc.render(oracle.camera_param(16 / 9, 4, 21), 72, 40)
+    assert_radiance(g["f32"], r["f32"])
+    assert np.array_equal(g["hit"], r["hit"])
+    check_counters(g["stats"], r["counters"], oracle)

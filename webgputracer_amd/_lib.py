@@ -35,11 +35,12 @@ class WgtStats(ctypes.Structure):
                 ("nan_rays", ctypes.c_uint64), ("node_visits", ctypes.c_uint64), ("tri_tests", ctypes.c_uint64),
                 ("pixels", ctypes.c_uint64), ("loop_wave_iters", ctypes.c_uint64),
                 ("loop_lane_iters", ctypes.c_uint64), ("trav_wave_steps", ctypes.c_uint64),
-                ("trav_lane_steps", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
-                ("pad", ctypes.c_float * 3)]
+                ("trav_lane_steps", ctypes.c_uint64), ("cyc_service", ctypes.c_uint64),
+                ("cyc_trav", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
+                ("trace_ms", ctypes.c_float), ("shade_ms", ctypes.c_float), ("iterations", ctypes.c_uint32)]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class WgtSceneInfo(ctypes.Structure):
@@ -56,7 +57,7 @@ class WgtSceneInfo(ctypes.Structure):
 EXPORTS = [
     "wgt_create", "wgt_destroy", "wgt_last_error", "wgt_version", "wgt_device_count",
     "wgt_upload_scene", "wgt_scene_info_get", "wgt_render_tile", "wgt_render_tiles_async",
-    "wgt_render_tiles_stats", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_stream",
+    "wgt_render_tiles_stats", "wgt_render_tiles_profile", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_stream",
     "wgt_scene_cornell", "wgt_make_triangles", "wgt_load_obj", "wgt_procedural_mesh",
     "wgt_write_obj", "wgt_write_png",
 ]
@@ -90,6 +91,7 @@ def lib():
         "wgt_render_tile": (I, [P, P, U32, U32, U32, U32, U32, U32, P, P, P, P]),
         "wgt_render_tiles_async": (I, [P, P, U32, U32, U32, U32, P, U32, P, P, P, P]),
         "wgt_render_tiles_stats": (I, [P, P, U32, U32, U32, U32, P, U32, P]),
+        "wgt_render_tiles_profile": (I, [P, P, U32, U32, U32, U32, P, U32, P]),
         "wgt_trace_rays": (I, [P, P, U32, P, P]),
         "wgt_trace_rays_async": (I, [P, P, U32, P, P, P]),
         "wgt_sync": (I, [P]),

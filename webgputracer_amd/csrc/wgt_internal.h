@@ -51,9 +51,38 @@ struct DevFrame {
   // kernel selection and phase-split thresholds (k_render_ps): switch from the
   // service to the traversal phase once >= ps_to_trav lanes traverse, and back
   // once <= ps_to_service lanes still traverse.
-  uint32_t kernel;  // 0 = phase-split (scenes with triangles), 1 = simple
+  uint32_t kernel;  // scenes with triangles: 0 = wavefront, 1 = simple, 2 = phase-split (default)
   uint32_t ps_to_trav, ps_to_service;
+  // wavefront: rays a slot may start per shade launch, slots per trace wave,
+  // idle lanes that trigger a refill from the wave's ray list
+  uint32_t wf_rays, wf_chunk, wf_refill;
 };
+
+// Wavefront path state, SoA over slots (one slot per pixel of the tile list).
+struct WfState {
+  uint32_t* seed;
+  uint32_t* k;
+  uint32_t* dp;    // depth | phase << 8
+  float* col;      // SoA x[n] y[n] z[n]
+  float* pc;
+  float* ro;
+  float* rd;
+  uint32_t* qprim;
+  float* qt;
+  uint32_t* res_i;  // closest triangle index or kNoHit
+  float* res_t;
+  unsigned long long* ctl;  // [0] slots done
+  uint32_t n;
+};
+size_t wf_state_bytes(uint32_t n);
+hipError_t wf_bind(void* mem, uint32_t n, unsigned long long* ctl, WfState& st);
+hipError_t launch_wf_init(const DevFrame& fr, const wgt_tile* tiles, const WfState& st, uchar4* out8,
+                          float4* out32, uint32_t* outhit, hipStream_t stream);
+hipError_t launch_wf_shade(const DevScene& sc, const DevFrame& fr, const wgt_tile* tiles,
+                           const WfState& st, uchar4* out8, float4* out32, uint32_t* outhit,
+                           unsigned long long* counters, hipStream_t stream);
+hipError_t launch_wf_trace(const DevScene& sc, const DevFrame& fr, const WfState& st,
+                           unsigned long long* counters, hipStream_t stream);
 
 enum {
   CNT_QUERIES = 0,
@@ -67,7 +96,9 @@ enum {
   CNT_LOOP_LANE,
   CNT_TRAV_WAVE,
   CNT_TRAV_LANE,
-  CNT_N = 12
+  CNT_CYC_SERVICE,  // s_memtime cycles per wave spent in each phase (instrumented pass)
+  CNT_CYC_TRAV,
+  CNT_N = 14
 };
 
 // Launchers implemented in wgt_kernels.hip

@@ -28,425 +28,9 @@
 // colour (contributing max(NaN, 0) = 0), so the LCG is advanced by 3*(50-depth)
 // steps in O(8) and the sample ends: bit-identical output, ~2/3 fewer queries on
 // the Cornell box.
-#include "wgt_geom.h"
-#include "wgt_internal.h"
+#include "wgt_device.h"
 
 namespace wgt {
-
-struct Hit {
-  float dist;
-  uint32_t prim;
-  bool emissive;
-  bool front_face;
-  f3 pos, norm, col;
-};
-
-__device__ __forceinline__ f3 xyz(float4 v) { return f3{v.x, v.y, v.z}; }
-
-__device__ __forceinline__ void hit_init(Hit& h) {
-  // HitInfo() zero-initialised, then path_tracer.wgsl:292-296
-  h.dist = kRayMax;
-  h.prim = kNoHit;
-  h.emissive = false;
-  h.front_face = false;
-  h.pos = f3{0.0f, 0.0f, 0.0f};
-  h.norm = f3{0.0f, 0.0f, 0.0f};
-  h.col = f3{0.0f, 0.0f, 0.0f};
-}
-
-// Accept quad q at parameter t with distance ray_dist (tail of intersect_quad).
-__device__ __forceinline__ void quad_accept(f3 o, f3 d, const float4* __restrict__ q, uint32_t id,
-                                            float t, float ray_dist, Hit& h) {
-  const f3 qn = xyz(q[3]);
-  const bool ff = dot(d, qn) < 0.0f;
-  const float4 c = q[5];
-  h.dist = ray_dist;
-  h.prim = id;
-  h.emissive = c.w > 0.0f;
-  h.front_face = ff;
-  h.pos = o + t * d;
-  h.norm = ff ? qn : -qn;
-  h.col = xyz(c);
-}
-
-// path_tracer.wgsl:314-338.  `qt` receives t of the accepted quad: the triangle
-// search bound, and what finalize needs to rebuild the quad hit bit for bit.
-__device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict__ q, uint32_t id,
-                                           Hit& h, float& qt) {
-  const f3 qn = xyz(q[3]);
-  const float denom = dot(qn, d);
-  if (fabs_w(denom) < kRayMin) return;
-  const float4 wd = q[4];
-  const float t = (wd.w - dot(qn, o)) / denom;
-  if (t < kRayMin || kRayMax < t) return;
-  const f3 pos = o + t * d;
-  const float ray_dist = distance(pos, o);
-  if (ray_dist >= h.dist) return;
-  const f3 hit_vec = pos - xyz(q[0]);
-  const f3 w = xyz(wd);
-  const float a = dot(w, cross(hit_vec, xyz(q[2])));
-  const float b = dot(w, cross(xyz(q[1]), hit_vec));
-  if ((a < 0.0f) || (1.0f < a) || (b < 0.0f) || (1.0f < b)) return;
-  quad_accept(o, d, q, id, t, ray_dist, h);
-  qt = t;
-}
-
-// path_tracer.wgsl:340-369 (sphere_uv is dead downstream: not computed)
-__device__ __forceinline__ void isect_sphere(f3 o, f3 d, const float4* __restrict__ s, uint32_t id,
-                                             Hit& h) {
-  const float4 cr = s[0];
-  const f3 center = xyz(cr);
-  const f3 oc = o - center;
-  const float a = dot(d, d);
-  const float half_b = dot(oc, d);
-  const float c = dot(oc, oc) - cr.w * cr.w;
-  const float disc = half_b * half_b - a * c;
-  if (disc < 0.0f) return;
-  const float sqrt_d = __builtin_sqrtf(disc);
-  float root = (-half_b - sqrt_d) / a;
-  if (root < kRayMin || kRayMax < root) {
-    root = (-half_b + sqrt_d) / a;
-    if (root < kRayMin || kRayMax < root) return;
-  }
-  const f3 pos = o + root * d;
-  const float ray_dist = distance(pos, o);
-  if (ray_dist >= h.dist) return;
-  const f3 sn = (pos - center) / cr.w;
-  const bool ff = dot(d, sn) < 0.0f;
-  const float4 col = s[1];
-  h.dist = ray_dist;
-  h.prim = id;
-  h.emissive = col.w > 0.0f;
-  h.front_face = ff;
-  h.pos = pos;
-  h.norm = ff ? sn : -sn;
-  h.col = xyz(col);
-}
-
-__device__ __forceinline__ void quad_scan(const DevScene& sc, f3 o, f3 d, Hit& h, float& qt) {
-  hit_init(h);
-  qt = kRayMax;
-  const uint32_t nlq = sc.n_lights + sc.n_quads;
-  for (uint32_t k = 0; k < nlq; ++k) isect_quad(o, d, sc.quads + 6 * k, k, h, qt);
-}
-
-// The quad part of a hit rebuilt from (prim, t): the same operations as isect_quad.
-__device__ __forceinline__ void quad_rebuild(const DevScene& sc, f3 o, f3 d, uint32_t prim, float t,
-                                             Hit& h) {
-  hit_init(h);
-  if (prim == kNoHit) return;
-  const f3 pos = o + t * d;
-  quad_accept(o, d, sc.quads + 6 * prim, prim, t, distance(pos, o), h);
-}
-
-__device__ __forceinline__ uint32_t last_prim(const DevScene& sc) {
-  return sc.n_lights + sc.n_quads + sc.n_tris + sc.n_spheres - 1u;
-}
-
-// A NaN ray's hit: the last sphere (every rejection test is false for NaN).
-__device__ __forceinline__ void nan_hit(const DevScene& sc, f3 o, f3 d, Hit& h) {
-  hit_init(h);
-  const uint32_t k = sc.n_spheres - 1;
-  isect_sphere(o, d, sc.spheres + 2 * k, sc.n_lights + sc.n_quads + sc.n_tris + k, h);
-}
-
-struct TravStats {
-  uint32_t nodes, tris, wave_steps, lane_steps;
-};
-
-// Counts one per wave (first active lane) and one per active lane.
-__device__ __forceinline__ void simt_count(uint32_t& wave, uint32_t& lane) {
-  const unsigned long long b = __ballot(1);
-  if (__lane_id() == (unsigned)(__ffsll((long long)b) - 1)) ++wave;
-  ++lane;
-}
-
-// Resumable BVH2 traversal: closest triangle = min (t, index) with t < bound (or
-// t <= bound and index < bi when bi = kNoHit).  Per-lane stack: kStackLds entries
-// in LDS (stride kBlock, conflict-free), overflow in private (scratch) memory.
-struct Trav {
-  f3 inv, ot;
-  float bt;
-  uint32_t bi;
-  int ref;
-  int sp;
-  uint32_t iters;
-  bool found;
-};
-
-__device__ __forceinline__ void trav_init(f3 o, f3 d, bool quad_hit, float qt, Trav& t) {
-  t.inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
-  t.ot = slab_offset(o, t.inv);
-  // a triangle must satisfy t < t_quad to beat a quad hit (ray_dist is monotone in t)
-  t.bt = quad_hit ? qt : kRayMax;
-  t.bi = quad_hit ? 0u : kNoHit;
-  t.ref = 0;
-  t.sp = 0;
-  t.iters = 0;
-  t.found = false;
-}
-
-// One node or one leaf.  Returns true when the traversal has finished.
-template <bool STATS>
-__device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& t,
-                                          int* __restrict__ lds, int* priv, TravStats& st) {
-  if (STATS) simt_count(st.wave_steps, st.lane_steps);
-  if (t.ref >= 0) {
-    const float4* __restrict__ n = sc.nodes + 4 * t.ref;
-    const float4 a = n[0], b = n[1], c = n[2], e = n[3];
-    if (STATS) st.nodes++;
-    float n0, f0, n1, f1;
-    slab(t.ot, t.inv, f3{a.x, a.z, c.x}, f3{a.y, a.w, c.y}, n0, f0);
-    slab(t.ot, t.inv, f3{b.x, b.z, c.z}, f3{b.y, b.w, c.w}, n1, f1);
-    const bool h0 = (n0 <= f0) & (n0 <= t.bt) & (f0 >= kRayMin);
-    const bool h1 = (n1 <= f1) & (n1 <= t.bt) & (f1 >= kRayMin);
-    const int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-    if (h0 && h1) {
-      const bool swap = n1 < n0;
-      const int nearr = swap ? r1 : r0;
-      const int farr = swap ? r0 : r1;
-      if (t.sp < kStackLds) lds[t.sp * kBlock] = farr;
-      else if (t.sp < kStackLds + kStackScratch) priv[t.sp - kStackLds] = farr;
-      ++t.sp;
-      t.ref = nearr;
-      return false;
-    }
-    if (h0) { t.ref = r0; return false; }
-    if (h1) { t.ref = r1; return false; }
-  } else {
-    const uint32_t first = leaf_first(t.ref), cnt = leaf_count(t.ref);
-    for (uint32_t k = 0; k < cnt; ++k) {
-      const float4* __restrict__ tp = sc.tris + 3 * (first + k);
-      const float4 A = tp[0], B = tp[1], C = tp[2];
-      if (STATS) st.tris++;
-      const f3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
-      float tt;
-      if (mt_test(o, d, v0, e1, e2, tt)) {
-        const uint32_t idx = __float_as_uint(A.w);
-        if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
-          f3 lo, hi;
-          tri_box(v0, e1, e2, lo, hi);
-          float bn, bf;
-          slab(t.ot, t.inv, lo, hi, bn, bf);
-          if (bn <= tt && tt <= bf) {
-            t.bt = tt;
-            t.bi = idx;
-            t.found = true;
-          }
-        }
-      }
-    }
-  }
-  if (t.sp == 0 || ++t.iters > sc.max_iters) return true;
-  --t.sp;
-  // pop: the LDS read is unconditional (ds_read); scratch only on overflow
-  int v = lds[(t.sp < kStackLds ? t.sp : kStackLds - 1) * kBlock];
-  if (t.sp >= kStackLds) v = priv[t.sp - kStackLds];
-  t.ref = v;
-  return false;
-}
-
-// Merge the triangle result into the quad hit, then scan the spheres: the end of
-// sample_hit (path_tracer.wgsl:305-309) with triangles between quads and spheres.
-__device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const Trav& t, Hit& h) {
-  const uint32_t nlq = sc.n_lights + sc.n_quads;
-  if (t.found) {
-    const f3 pos = o + t.bt * d;
-    const float ray_dist = distance(pos, o);
-    if (!(ray_dist >= h.dist)) {
-      const float4 s0 = sc.tshade[2 * t.bi], s1 = sc.tshade[2 * t.bi + 1];
-      const f3 fn = xyz(s0);
-      const bool ff = dot(d, fn) < 0.0f;
-      h.dist = ray_dist;
-      h.prim = nlq + t.bi;
-      h.emissive = s0.w > 0.0f;
-      h.front_face = ff;
-      h.pos = pos;
-      h.norm = ff ? fn : -fn;
-      h.col = xyz(s1);
-    }
-  }
-  for (uint32_t k = 0; k < sc.n_spheres; ++k)
-    isect_sphere(o, d, sc.spheres + 2 * k, nlq + sc.n_tris + k, h);
-}
-
-// Full sample_hit for one ray (k_trace, k_render).
-template <bool TRIS, bool STATS>
-__device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* __restrict__ lds,
-                                           int* priv, Hit& h, TravStats& st) {
-  if (has_nan(o) || has_nan(d)) {
-    nan_hit(sc, o, d, h);
-    return;
-  }
-  float qt;
-  quad_scan(sc, o, d, h, qt);
-  Trav t;
-  trav_init(o, d, h.prim != kNoHit, qt, t);
-  if (TRIS) {
-    while (!trav_step<STATS>(sc, o, d, t, lds, priv, st)) {
-    }
-  }
-  finish_hit(sc, o, d, t, h);
-}
-
-struct Light {
-  f3 pos, right, up;
-};
-
-// raytrace() after sample_hit (path_tracer.wgsl:267-287).  Returns path.end.
-__device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const Hit& h, int depth,
-                                      uint32_t& seed, f3& ro, f3& rd, f3& pc) {
-  if (h.emissive) {
-    if (depth != 0) {
-      const float ff = h.front_face ? 1.0f : 0.0f;
-      pc = (ff * h.col) * pc;
-    } else {
-      pc = h.col;
-    }
-    return true;
-  }
-  // sample_direction (path_tracer.wgsl:146-154)
-  const f3 w = normalize(h.norm);  // onb.w of build_onb_from_w(hit.norm)
-  f3 sdir;
-  if (rand_next(seed) > 0.5f) {
-    // sample_from_cosine: build_onb_from_w (:133-140) + rand_cos_dir (:123-131)
-    const f3 a = (sign_w(w.x) * w.x) > 0.9f ? f3{0.0f, 1.0f, 0.0f} : f3{1.0f, 0.0f, 0.0f};
-    const f3 v = normalize(cross(w, a));
-    const f3 u = cross(w, v);
-    const float r1 = rand_next(seed);
-    const float r2 = rand_next(seed);
-    const float z = __builtin_sqrtf(1.0f - r2);
-    const float phi = 2.0f * kPI * r1;
-    float sphi, cphi;
-    sincos_w(phi, sphi, cphi);
-    const float sr2 = __builtin_sqrtf(r2);
-    const float lx2 = cphi * sr2;
-    const float ly2 = sphi * sr2;
-    sdir = (lx2 * u + ly2 * v) + z * w;
-  } else {
-    // sample_from_light (:163-168), not normalised
-    const float r1 = rand_next(seed);
-    const float r2 = rand_next(seed);
-    sdir = ((L.pos + r1 * L.right) + r2 * L.up) - h.pos;
-  }
-  // mixture_pdf (:191-193) = 0.5*cosine_pdf + 0.5*light_area_pdf
-  const float len = length(sdir);
-  const f3 nd = sdir / len;  // normalize(dir): shared by cosine_pdf, the light cosine and :282
-  const float cs = dot(nd, w);
-  const float cpdf = cs <= 0.0f ? 0.0f : cs * k_1_PI;
-  const float dist2 = len * len;
-  const float light_cosine = fabs_w(nd.y) + kRayMin;
-  const float lpdf = dist2 / (light_cosine * sc.light_area);
-  const float pdf_val = 0.5f * cpdf + 0.5f * lpdf;
-  // scattering_pdf (:217-220) normalises the already normalised direction again
-  const f3 nd2 = normalize(nd);
-  const float cs2 = dot(h.norm, nd2);
-  const float spdf = cs2 < 0.0f ? 0.0f : cs2 * k_1_PI;
-  pc = (spdf * (pc * h.col)) / pdf_val;
-  ro = h.pos;
-  rd = nd;
-  return false;
-}
-
-__device__ __forceinline__ uint8_t unorm8(float x) {
-  float c = max0(x);
-  c = c < 1.0f ? c : 1.0f;
-  return (uint8_t)__builtin_floorf(c * 255.0f + 0.5f);
-}
-
-// Per-pixel state shared by both kernels.
-struct Pixel {
-  uint32_t x, y;
-  uint32_t seed;
-  uint32_t k, si, sj;  // sample index and its (s_i, s_j)
-  f3 col;
-  uint32_t hit0;
-};
-
-struct Counters {
-  uint32_t q, tr, nan, lw, ll;
-};
-
-// Pixel of this lane, or false if the lane has none.
-__device__ __forceinline__ bool pixel_setup(const DevFrame& fr, const wgt_tile* __restrict__ tiles,
-                                            uint32_t& tile, uint32_t& lx, uint32_t& ly, Pixel& px) {
-  const uint32_t bx = (fr.tw + 7u) >> 3, by = (fr.th + 7u) >> 3;
-  const uint32_t bpt = bx * by;
-  tile = blockIdx.x / bpt;
-  const uint32_t rem = blockIdx.x - tile * bpt;
-  lx = (rem % bx) * 8u + (threadIdx.x & 7u);
-  ly = (rem / bx) * 8u + (threadIdx.x >> 3);
-  if (tile >= fr.n_tiles || lx >= fr.tw || ly >= fr.th) return false;
-  const wgt_tile td = tiles[tile];
-  px.x = td.x0 + lx;
-  px.y = td.y0 + ly;
-  if (px.x >= fr.W || px.y >= fr.H) return false;  // path_tracer.wgsl:377
-  px.seed = px.x + px.y * fr.W + td.seed * fr.W * fr.H;  // path_tracer.wgsl:378
-  px.k = px.si = px.sj = 0;
-  px.col = f3{0.0f, 0.0f, 0.0f};
-  px.hit0 = kNoHit;
-  return true;
-}
-
-// setup_camera_ray + pixel_sample_square (path_tracer.wgsl:232-262) for sample px.k
-__device__ __forceinline__ void camera_ray(const DevFrame& fr, Pixel& px, f3& ro, f3& rd) {
-  const f3 origin = f3{fr.ox, fr.oy, fr.oz};
-  const f3 du = f3{fr.dux, fr.duy, fr.duz};
-  const f3 dv = f3{fr.dvx, fr.dvy, fr.dvz};
-  const f3 pixel_center = (f3{fr.pox, fr.poy, fr.poz} + (float)px.x * du) + (float)px.y * dv;
-  const float sx = -0.5f + fr.recip_sqrt_spp * ((float)px.si + rand_next(px.seed));
-  const float sy = -0.5f + fr.recip_sqrt_spp * ((float)px.sj + rand_next(px.seed));
-  const f3 pixel_sample = pixel_center + (sx * du + sy * dv);
-  ro = origin;
-  rd = pixel_sample - origin;
-}
-
-// col += max(path.col, 0) / f32(spp) (path_tracer.wgsl:393) and advance to the next sample
-__device__ __forceinline__ void end_sample(const DevFrame& fr, Pixel& px, f3 pc) {
-  px.col = px.col + f3{max0(pc.x) / fr.fspp, max0(pc.y) / fr.fspp, max0(pc.z) / fr.fspp};
-  ++px.k;
-  if (++px.si == fr.sqrt_spp) { px.si = 0; ++px.sj; }
-}
-
-// NaN-absorbed for the rest of the path: 3 rand() per remaining bounce, colour NaN.
-template <bool STATS>
-__device__ __forceinline__ void skip_nan_path(const DevScene& sc, const DevFrame& fr, Pixel& px,
-                                              int depth, Counters& c) {
-  px.seed = lcg_jump(px.seed, 3u * (uint32_t)(kRayDepth - depth));
-  if (STATS) {
-    c.q += (uint32_t)(kRayDepth - depth);
-    c.nan += (uint32_t)(kRayDepth - depth);
-  }
-  if (px.k == 0 && depth == 0) px.hit0 = last_prim(sc);
-  // col += max(NaN, 0) / spp == col + 0
-  ++px.k;
-  if (++px.si == fr.sqrt_spp) { px.si = 0; ++px.sj; }
-}
-
-__device__ __forceinline__ void write_pixel(const DevFrame& fr, uint32_t tile, uint32_t lx,
-                                            uint32_t ly, const Pixel& px, uchar4* out8, float4* out32,
-                                            uint32_t* outhit) {
-  const size_t o = ((size_t)tile * fr.th + ly) * fr.tw + lx;
-  if (out32) out32[o] = make_float4(px.col.x, px.col.y, px.col.z, 1.0f);
-  if (out8) out8[o] = make_uchar4(unorm8(px.col.x), unorm8(px.col.y), unorm8(px.col.z), 255);
-  if (outhit) outhit[o] = px.hit0;
-}
-
-__device__ __forceinline__ void flush_counters(unsigned long long* __restrict__ counters,
-                                               const Counters& c, const TravStats& st,
-                                               uint32_t nsamp) {
-  atomicAdd(&counters[CNT_QUERIES], (unsigned long long)c.q);
-  atomicAdd(&counters[CNT_TRACED], (unsigned long long)c.tr);
-  atomicAdd(&counters[CNT_SAMPLES], (unsigned long long)nsamp);
-  atomicAdd(&counters[CNT_NAN], (unsigned long long)c.nan);
-  atomicAdd(&counters[CNT_NODES], (unsigned long long)st.nodes);
-  atomicAdd(&counters[CNT_TRIS], (unsigned long long)st.tris);
-  atomicAdd(&counters[CNT_PIXELS], 1ull);
-  atomicAdd(&counters[CNT_LOOP_WAVE], (unsigned long long)c.lw);
-  atomicAdd(&counters[CNT_LOOP_LANE], (unsigned long long)c.ll);
-  atomicAdd(&counters[CNT_TRAV_WAVE], (unsigned long long)st.wave_steps);
-  atomicAdd(&counters[CNT_TRAV_LANE], (unsigned long long)st.lane_steps);
-}
 
 template <bool TRIS, bool STATS>
 __global__ void __launch_bounds__(kBlock)
@@ -518,9 +102,11 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   uint32_t q_prim = kNoHit;  // quad part of the pending hit, rebuilt at finalisation
   float q_t = kRayMax;
   bool done = nsamp == 0, trav = false, pending = false;
+  uint64_t cyc_svc = 0, cyc_trav = 0;
 
   for (;;) {
     // ------------------------------------------------------------ service phase
+    uint64_t t_phase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
       const bool need = !trav && !done;
       if (!__any(need)) break;
@@ -582,6 +168,11 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       }
       if ((uint32_t)__popcll(__ballot(trav)) >= fr.ps_to_trav) break;
     }
+    if (STATS) {
+      const uint64_t now = __builtin_amdgcn_s_memtime();
+      cyc_svc += now - t_phase;
+      t_phase = now;
+    }
     if (!__any(!done)) break;
     // --------------------------------------------------------- traversal phase
     for (;;) {
@@ -593,9 +184,16 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       if (ntrav == 0) break;
       if (ntrav <= fr.ps_to_service && __any(!trav && !done)) break;
     }
+    if (STATS) cyc_trav += __builtin_amdgcn_s_memtime() - t_phase;
   }
   write_pixel(fr, tile, lx, ly, px, out8, out32, outhit);
-  if (STATS) flush_counters(counters, c, st, nsamp);
+  if (STATS) {
+    flush_counters(counters, c, st, nsamp);
+    if (__lane_id() == (unsigned)(__ffsll((long long)__ballot(1)) - 1)) {
+      atomicAdd(&counters[CNT_CYC_SERVICE], (unsigned long long)cyc_svc);
+      atomicAdd(&counters[CNT_CYC_TRAV], (unsigned long long)cyc_trav);
+    }
+  }
 }
 
 template <bool TRIS>
@@ -624,7 +222,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
   const dim3 grid((uint32_t)blocks), block(kBlock);
   const bool tris = sc.n_tris > 0;
-  const bool ps = tris && fr.kernel != 1;
+  const bool ps = tris && fr.kernel == 2;
   if (counters) {
     if (ps) k_render_ps<true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
     else if (tris) k_render<true, true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);

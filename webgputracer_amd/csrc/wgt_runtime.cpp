@@ -45,6 +45,10 @@ struct wgt_ctx {
   wgt_scene_info info{};
   // scratch for the synchronous entry points
   DevBuf tiles, out8, out32, hit, counters, rays, prim, dist;
+  // wavefront path state + completion counter (device) and its pinned mirror
+  DevBuf wf, ctl;
+  unsigned long long* ctl_host = nullptr;
+  std::vector<hipEvent_t> evpool;  // per-launch timing (profile runs only)
 };
 
 namespace {
@@ -120,9 +124,12 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.sqrt_spp = (uint32_t)__builtin_sqrtf((float)cam.spp);
   fr.W = W;
   fr.H = H;
-  fr.kernel = env_u32("WGT_KERNEL", 0);
-  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 32);
-  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 16);
+  fr.kernel = env_u32("WGT_KERNEL", 2);
+  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 24);
+  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 8);
+  fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
+  fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
+  fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
   return fr;
 }
 
@@ -150,6 +157,99 @@ void fill_stats(const unsigned long long* c, wgt_stats* s) {
   s->loop_lane_iters = c[CNT_LOOP_LANE];
   s->trav_wave_steps = c[CNT_TRAV_WAVE];
   s->trav_lane_steps = c[CNT_TRAV_LANE];
+  s->cyc_service = c[CNT_CYC_SERVICE];
+  s->cyc_trav = c[CNT_CYC_TRAV];
+}
+
+
+// Times accumulated over the launches of one frame (profile runs only).
+struct FrameTiming {
+  float trace_ms = 0.0f, shade_ms = 0.0f, total_ms = 0.0f;
+  uint32_t iterations = 0;
+};
+
+hipEvent_t pool_event(wgt_ctx* ctx, size_t i) {
+  while (ctx->evpool.size() <= i) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    ctx->evpool.push_back(e);
+  }
+  return ctx->evpool[i];
+}
+
+// Render the tile list: the wavefront loop for scenes with triangles (default),
+// otherwise one megakernel launch.  Blocks until the frame is complete when the
+// wavefront loop runs (it polls a completion counter every few iterations).
+int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, uchar4* out8, float4* out32,
+                 uint32_t* outhit, unsigned long long* counters, hipStream_t s, FrameTiming* timing) {
+  const bool wavefront = ctx->sc.n_tris > 0 && fr.kernel == 0;
+  if (!wavefront) {
+    hipEvent_t e0 = timing ? pool_event(ctx, 0) : nullptr, e1 = timing ? pool_event(ctx, 1) : nullptr;
+    if (timing && (!e0 || !e1)) return fail(ctx, WGT_E_HIP, "hipEventCreate failed");
+    if (timing) WGT_HIP(ctx, hipEventRecord(e0, s));
+    WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, s));
+    if (timing) {
+      WGT_HIP(ctx, hipEventRecord(e1, s));
+      WGT_HIP(ctx, hipEventSynchronize(e1));
+      WGT_HIP(ctx, hipEventElapsedTime(&timing->total_ms, e0, e1));
+      timing->trace_ms = timing->total_ms;
+      timing->iterations = 1;
+    }
+    return WGT_OK;
+  }
+  const uint64_t n64 = (uint64_t)fr.tw * fr.th * fr.n_tiles;
+  if (n64 == 0) return WGT_OK;
+  if (n64 > 0x7fffffffull) return fail(ctx, WGT_E_INVALID, "too many pixels in one launch");
+  const uint32_t n = (uint32_t)n64;
+  int rc;
+  if ((rc = ensure(ctx, ctx->wf, wf_state_bytes(n)))) return rc;
+  if ((rc = ensure(ctx, ctx->ctl, 256))) return rc;
+  if (!ctx->ctl_host) WGT_HIP(ctx, hipHostMalloc((void**)&ctx->ctl_host, 256, hipHostMallocDefault));
+  WfState st;
+  (void)wf_bind(ctx->wf.p, n, (unsigned long long*)ctx->ctl.p, st);
+  WGT_HIP(ctx, hipMemsetAsync(ctx->ctl.p, 0, 8, s));
+  size_t ev = 0;
+  auto mark = [&]() -> hipEvent_t {
+    hipEvent_t e = pool_event(ctx, ev++);
+    if (e) (void)hipEventRecord(e, s);
+    return e;
+  };
+  if (timing) mark();
+  WGT_HIP(ctx, launch_wf_init(fr, d_tiles, st, out8, out32, outhit, s));
+  // every slot advances by >= 1 traced ray per iteration; bound the loop anyway
+  const uint64_t nsamp = (uint64_t)fr.sqrt_spp * fr.sqrt_spp;
+  const uint64_t max_iter = nsamp * (uint64_t)(kRayDepth + 1) + 64;
+  const uint32_t check_every = env_u32("WGT_WF_CHECK", 32);
+  uint64_t it = 0;
+  for (;;) {
+    if (timing) mark();
+    WGT_HIP(ctx, launch_wf_shade(ctx->sc, fr, d_tiles, st, out8, out32, outhit, counters, s));
+    if (timing) mark();
+    WGT_HIP(ctx, launch_wf_trace(ctx->sc, fr, st, counters, s));
+    ++it;
+    if (it % check_every == 0 || it >= max_iter) {
+      WGT_HIP(ctx, hipMemcpyAsync(ctx->ctl_host, ctx->ctl.p, 8, hipMemcpyDeviceToHost, s));
+      WGT_HIP(ctx, hipStreamSynchronize(s));
+      if (ctx->ctl_host[0] >= n) break;
+      if (it >= max_iter) return fail(ctx, WGT_E_HIP, "wavefront loop did not converge");
+    }
+  }
+  if (timing) {
+    mark();
+    WGT_HIP(ctx, hipStreamSynchronize(s));
+    // events: [0] init start, then (shade start, trace start) per iteration, [last] end
+    float ms = 0.0f;
+    for (uint64_t i = 0; i < it; ++i) {
+      hipEvent_t a = ctx->evpool[1 + 2 * i], b = ctx->evpool[2 + 2 * i], c = ctx->evpool[3 + 2 * i];
+      WGT_HIP(ctx, hipEventElapsedTime(&ms, a, b));
+      timing->shade_ms += ms;
+      WGT_HIP(ctx, hipEventElapsedTime(&ms, b, c));
+      timing->trace_ms += ms;
+    }
+    WGT_HIP(ctx, hipEventElapsedTime(&timing->total_ms, ctx->evpool[0], ctx->evpool[ev - 1]));
+    timing->iterations = (uint32_t)it;
+  }
+  return WGT_OK;
 }
 
 }  // namespace
@@ -203,6 +303,9 @@ void wgt_destroy(wgt_ctx* ctx) {
   if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
   free_buf(ctx->tiles); free_buf(ctx->out8); free_buf(ctx->out32); free_buf(ctx->hit);
   free_buf(ctx->counters); free_buf(ctx->rays); free_buf(ctx->prim); free_buf(ctx->dist);
+  free_buf(ctx->wf); free_buf(ctx->ctl);
+  if (ctx->ctl_host) (void)hipHostFree(ctx->ctl_host);
+  for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
   if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
@@ -317,9 +420,8 @@ int wgt_render_tiles_async(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W
   fr.th = th;
   fr.n_tiles = n_tiles;
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-  WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, (uchar4*)d_rgba8, (float4*)d_rgba32f, d_hit_id,
-                             nullptr, s));
-  return WGT_OK;
+  return render_frame(ctx, fr, d_tiles, (uchar4*)d_rgba8, (float4*)d_rgba32f, d_hit_id, nullptr, s,
+                      nullptr);
 }
 
 int wgt_render_tiles_stats(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H,
@@ -338,12 +440,38 @@ int wgt_render_tiles_stats(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W
   fr.tw = tw;
   fr.th = th;
   fr.n_tiles = n_tiles;
-  WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, nullptr, nullptr, nullptr,
-                             (unsigned long long*)ctx->counters.p, ctx->stream));
+  if ((rc = render_frame(ctx, fr, d_tiles, nullptr, nullptr, nullptr,
+                         (unsigned long long*)ctx->counters.p, ctx->stream, nullptr)))
+    return rc;
   unsigned long long c[CNT_N];
   WGT_HIP(ctx, hipMemcpyAsync(c, ctx->counters.p, sizeof c, hipMemcpyDeviceToHost, ctx->stream));
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   fill_stats(c, stats);
+  return WGT_OK;
+}
+
+int wgt_render_tiles_profile(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H,
+                             uint32_t tw, uint32_t th, const wgt_tile* d_tiles, uint32_t n_tiles,
+                             wgt_stats* stats) {
+  int rc = check_render_args(ctx, cam, W, H, tw, th);
+  if (rc) return rc;
+  if (!stats) return fail(ctx, WGT_E_INVALID, "null stats");
+  std::memset(stats, 0, sizeof *stats);
+  if (n_tiles == 0) return WGT_OK;
+  if (!d_tiles) return fail(ctx, WGT_E_INVALID, "null tile list");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  DevFrame fr = make_frame(*cam, W, H);
+  fr.tw = tw;
+  fr.th = th;
+  fr.n_tiles = n_tiles;
+  FrameTiming timing;
+  if ((rc = render_frame(ctx, fr, d_tiles, nullptr, nullptr, nullptr, nullptr, ctx->stream, &timing)))
+    return rc;
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  stats->kernel_ms = timing.total_ms;
+  stats->trace_ms = timing.trace_ms;
+  stats->shade_ms = timing.shade_ms;
+  stats->iterations = timing.iterations;
   return WGT_OK;
 }
 
@@ -372,12 +500,12 @@ int wgt_render_tile(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint3
   fr.tw = tw;
   fr.th = th;
   fr.n_tiles = 1;
-  WGT_HIP(ctx, hipEventRecord(ctx->ev0, ctx->stream));
-  WGT_HIP(ctx, launch_render(ctx->sc, fr, (const wgt_tile*)ctx->tiles.p,
-                             rgba8_out ? (uchar4*)ctx->out8.p : nullptr,
-                             rgba32f_out ? (float4*)ctx->out32.p : nullptr,
-                             hit_id_out ? (uint32_t*)ctx->hit.p : nullptr, nullptr, ctx->stream));
-  WGT_HIP(ctx, hipEventRecord(ctx->ev1, ctx->stream));
+  FrameTiming timing;
+  if ((rc = render_frame(ctx, fr, (const wgt_tile*)ctx->tiles.p, rgba8_out ? (uchar4*)ctx->out8.p : nullptr,
+                         rgba32f_out ? (float4*)ctx->out32.p : nullptr,
+                         hit_id_out ? (uint32_t*)ctx->hit.p : nullptr, nullptr, ctx->stream,
+                         stats ? &timing : nullptr)))
+    return rc;
   if (rgba8_out)
     WGT_HIP(ctx, hipMemcpyAsync(rgba8_out, ctx->out8.p, npx * 4, hipMemcpyDeviceToHost, ctx->stream));
   if (rgba32f_out)
@@ -386,11 +514,12 @@ int wgt_render_tile(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint3
     WGT_HIP(ctx, hipMemcpyAsync(hit_id_out, ctx->hit.p, npx * 4, hipMemcpyDeviceToHost, ctx->stream));
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (stats) {
-    float ms = 0.0f;
-    WGT_HIP(ctx, hipEventElapsedTime(&ms, ctx->ev0, ctx->ev1));
     rc = wgt_render_tiles_stats(ctx, cam, W, H, tw, th, (const wgt_tile*)ctx->tiles.p, 1, stats);
     if (rc) return rc;
-    stats->kernel_ms = ms;
+    stats->kernel_ms = timing.total_ms;
+    stats->trace_ms = timing.trace_ms;
+    stats->shade_ms = timing.shade_ms;
+    stats->iterations = timing.iterations;
   }
   return WGT_OK;
 }

@@ -175,6 +175,13 @@ class Context:
                                                    n_tiles, ctypes.byref(st)))
         return st.as_dict()
 
+    def render_tiles_profile(self, cam, W, H, tw, th, d_tiles, n_tiles):
+        st = WgtStats()
+        cam = np.ascontiguousarray(cam, CAMERA_DTYPE)
+        self._check(self._L.wgt_render_tiles_profile(self.h, ptr(cam), W, H, tw, th, ctypes.c_void_p(d_tiles),
+                                                     n_tiles, ctypes.byref(st)))
+        return st.as_dict()
+
     def trace_rays(self, start, direction):
         start = np.asarray(start, np.float32).reshape(-1, 3)
         direction = np.asarray(direction, np.float32).reshape(-1, 3)
