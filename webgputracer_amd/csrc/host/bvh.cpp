@@ -42,6 +42,16 @@ struct Prim {
 };
 
 constexpr int kBins = 32;
+
+// Depth of a median-split subtree over `count` primitives (leaves <= kLeafMax).
+uint32_t MedianDepth(uint32_t count) {
+  uint32_t d = 0;
+  while (count > (uint32_t)kLeafMax) {
+    count = (count + 1) / 2;
+    ++d;
+  }
+  return d;
+}
 constexpr double kCostTrav = 1.0;
 constexpr double kCostTri = 1.0;
 
@@ -66,8 +76,11 @@ class Builder {
     if (count == 1) return MakeLeaf(begin, count, box);
 
     uint32_t mid = begin;
-    bool median = depth + 24 >= limit_;
-    if (!median) {
+    // Depth guarantee: every leaf at depth <= limit_ (the traversal stack holds at
+    // most `depth` entries).  Invariant: depth + MedianDepth(count) <= limit_; an SAH
+    // split is taken only if both children keep it, otherwise the median split does.
+    bool median = false;
+    {
       double best = std::numeric_limits<double>::infinity();
       int best_axis = -1, best_bin = -1;
       const double parea = box.area();
@@ -119,6 +132,7 @@ class Builder {
         });
         mid = (uint32_t)(it - prims_.begin());
         if (mid == begin || mid == end) median = true;
+        else if (depth + 1 + MedianDepth(std::max(mid - begin, end - mid)) > limit_) median = true;
       } else if (count <= (uint32_t)kLeafMax) {
         return MakeLeaf(begin, count, box);
       } else {
@@ -126,7 +140,7 @@ class Builder {
       }
     }
     if (median) {
-      if (count <= (uint32_t)kLeafMax && depth + 2 >= limit_) return MakeLeaf(begin, count, box);
+      if (count <= (uint32_t)kLeafMax) return MakeLeaf(begin, count, box);
       int axis = 0;
       for (int c = 1; c < 3; ++c)
         if (cb.hi[c] - cb.lo[c] > cb.hi[axis] - cb.lo[axis]) axis = c;
@@ -196,6 +210,10 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, Bv
     }
   }
   out.nodes.reserve((size_t)16 * 2 * (n / 2 + 1));
+  if (MedianDepth(n) > max_depth_limit) {
+    err = "BuildBvh: too many triangles for depth limit " + std::to_string(max_depth_limit);
+    return false;
+  }
   Builder b(prims, out, max_depth_limit);
   Box root_box;
   const int root = b.Build(0, n, 0, root_box);

@@ -139,7 +139,7 @@ __device__ __forceinline__ void simt_count(uint32_t& wave, uint32_t& lane) {
 
 // Resumable BVH2 traversal: closest triangle = min (t, index) with t < bound (or
 // t <= bound and index < bi when bi = kNoHit).  Per-lane stack: kStackLds entries
-// in LDS (stride kBlock, conflict-free), overflow in private (scratch) memory.
+// in LDS (stride kBlock, conflict-free).
 struct Trav {
   f3 inv, ot;
   float bt;
@@ -164,24 +164,20 @@ __device__ __forceinline__ void trav_init(f3 o, f3 d, bool quad_hit, float qt, T
   t.found = false;
 }
 
-// Descend into a child reference: internal node, or open a leaf's triangle range.
-__device__ __forceinline__ void trav_enter(Trav& t, int ref) {
-  if (ref >= 0) {
-    t.ref = ref;
-  } else {
-    t.lf = leaf_first(ref);
-    t.le = t.lf + leaf_count(ref);
-  }
-}
 
 // One BVH node OR one triangle per call (a leaf is opened as a range and its
 // triangles are tested one per step), so every lane's step costs about the same
-// and a wave never pays for an 8-triangle leaf loop at every step.  Returns true
-// when the traversal has finished.
+// and a wave never pays for an 8-triangle leaf loop at every step.  The stack
+// lives in LDS only: the builder bounds the BVH depth by STACK (kMaxBvhDepth), so
+// it cannot overflow.  Push / pop / descend are written as selects around one
+// leaf-or-node branch to keep the exec-mask bookkeeping small.  Returns true when
+// the traversal has finished.
 template <bool STATS, int STACK = kStackLds>
 __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& t,
-                                          int* __restrict__ lds, int* priv, TravStats& st) {
+                                          int* __restrict__ lds, TravStats& st) {
   if (STATS) simt_count(st.wave_steps, st.lane_steps);
+  bool pop;
+  int next = 0;
   if (t.lf < t.le) {
     const float4* __restrict__ tp = sc.tris + 3 * t.lf;
     const float4 A = tp[0], B = tp[1], C = tp[2];
@@ -202,7 +198,9 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
         }
       }
     }
-    if (++t.lf < t.le) return false;
+    ++t.lf;
+    if (t.lf < t.le) return false;
+    pop = true;
   } else {
     const float4* __restrict__ n = sc.nodes + 4 * t.ref;
     const float4 a = n[0], b = n[1], c = n[2], e = n[3];
@@ -213,27 +211,23 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
     const bool h0 = (n0 <= f0) & (n0 <= t.bt) & (f0 >= kRayMin);
     const bool h1 = (n1 <= f1) & (n1 <= t.bt) & (f1 >= kRayMin);
     const int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-    if (h0 && h1) {
-      const bool swap = n1 < n0;
-      const int nearr = swap ? r1 : r0;
-      const int farr = swap ? r0 : r1;
-      if (t.sp < STACK) lds[t.sp * kBlock] = farr;
-      else if (t.sp < STACK + kStackScratch) priv[t.sp - STACK] = farr;
-      ++t.sp;
-      trav_enter(t, nearr);
-      return false;
-    }
-    if (h0 || h1) {
-      trav_enter(t, h0 ? r0 : r1);
-      return false;
-    }
+    const bool both = h0 & h1;
+    const bool first1 = both ? (n1 < n0) : h1;  // descend into child 1
+    next = first1 ? r1 : r0;
+    if (both) lds[t.sp * kBlock] = first1 ? r0 : r1;
+    t.sp += both ? 1 : 0;
+    pop = !(h0 | h1);
   }
-  if (t.sp == 0 || ++t.iters > sc.max_iters) return true;
-  --t.sp;
-  // pop: the LDS read is unconditional (ds_read); scratch only on overflow
-  int v = lds[(t.sp < STACK ? t.sp : STACK - 1) * kBlock];
-  if (t.sp >= STACK) v = priv[t.sp - STACK];
-  trav_enter(t, v);
+  if (pop) {
+    if (t.sp == 0 || ++t.iters > sc.max_iters) return true;
+    --t.sp;
+    next = lds[t.sp * kBlock];
+  }
+  const bool leaf = next < 0;
+  const uint32_t lfirst = leaf_first(next);
+  t.lf = leaf ? lfirst : t.lf;
+  t.le = leaf ? lfirst + leaf_count(next) : t.le;
+  t.ref = leaf ? t.ref : next;
   return false;
 }
 
@@ -264,7 +258,7 @@ __device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const
 // Full sample_hit for one ray (k_trace, k_render).
 template <bool TRIS, bool STATS>
 __device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* __restrict__ lds,
-                                           int* priv, Hit& h, TravStats& st) {
+                                           Hit& h, TravStats& st) {
   if (has_nan(o) || has_nan(d)) {
     nan_hit(sc, o, d, h);
     return;
@@ -274,7 +268,7 @@ __device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* 
   Trav t;
   trav_init(o, d, h.prim != kNoHit, qt, t);
   if (TRIS) {
-    while (!trav_step<STATS>(sc, o, d, t, lds, priv, st)) {
+    while (!trav_step<STATS>(sc, o, d, t, lds, st)) {
     }
   }
   finish_hit(sc, o, d, t, h);

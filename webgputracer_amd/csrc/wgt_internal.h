@@ -19,9 +19,11 @@
 namespace wgt {
 
 constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
-constexpr int kStackLds = 24;     // per-lane traversal stack entries in LDS (6 KB/wave)
-constexpr int kStackScratch = 64; // overflow entries in private (scratch) memory
-constexpr int kMaxBvhDepth = kStackLds + kStackScratch - 2;
+// Per-lane traversal stack entries in LDS (6 KB per wave).  The BVH builder
+// guarantees depth <= kMaxBvhDepth, and the stack never holds more than the depth,
+// so the stack cannot overflow and needs no spill path.
+constexpr int kStackLds = 24;
+constexpr int kMaxBvhDepth = kStackLds;
 
 struct DevScene {
   const float4* __restrict__ quads;   // n_lights + n_quads records

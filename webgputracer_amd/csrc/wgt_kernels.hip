@@ -42,7 +42,6 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
   Pixel px;
   if (!pixel_setup(fr, tiles, tile, lx, ly, px)) return;
   int* lds = s_stack + threadIdx.x;
-  int priv[kStackScratch];
   const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
   const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
   f3 ro{}, rd{}, pc{};
@@ -63,7 +62,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
       continue;
     }
     Hit h;
-    sample_hit<TRIS, STATS>(sc, ro, rd, lds, priv, h, st);
+    sample_hit<TRIS, STATS>(sc, ro, rd, lds, h, st);
     if (STATS) {
       ++c.q;
       if (nanray) ++c.nan; else ++c.tr;
@@ -91,7 +90,6 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   Pixel px;
   if (!pixel_setup(fr, tiles, tile, lx, ly, px)) return;
   int* lds = s_stack + threadIdx.x;
-  int priv[kStackScratch];
   const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
   const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
   f3 ro{}, rd{}, pc{};
@@ -161,7 +159,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           trav_init(ro, rd, q_prim != kNoHit, q_t, t);
           // the root node is tested here: rays that miss both root children never
           // enter the traversal phase
-          if (trav_step<STATS>(sc, ro, rd, t, lds, priv, st)) pending = true;
+          if (trav_step<STATS>(sc, ro, rd, t, lds, st)) pending = true;
           else trav = true;
           break;
         }
@@ -176,7 +174,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
     if (!__any(!done)) break;
     // --------------------------------------------------------- traversal phase
     for (;;) {
-      if (trav && trav_step<STATS>(sc, ro, rd, t, lds, priv, st)) {
+      if (trav && trav_step<STATS>(sc, ro, rd, t, lds, st)) {
         trav = false;
         pending = true;
       }
@@ -203,12 +201,11 @@ k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __res
   __shared__ int s_stack[kStackLds * kBlock];
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
-  int priv[kStackScratch];
   const f3 o = f3{rays[i], rays[(size_t)n + i], rays[2 * (size_t)n + i]};
   const f3 d = f3{rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]};
   Hit h;
   TravStats st{0u, 0u, 0u, 0u};
-  sample_hit<TRIS, false>(sc, o, d, s_stack + threadIdx.x, priv, h, st);
+  sample_hit<TRIS, false>(sc, o, d, s_stack + threadIdx.x, h, st);
   prim[i] = h.prim;
   dist[i] = h.dist;
 }

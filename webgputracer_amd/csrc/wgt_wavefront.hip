@@ -29,7 +29,7 @@ namespace wgt {
 enum : uint32_t { PH_NEED = 0u, PH_WAIT = 1u, PH_DONE = 2u };
 
 constexpr int kWfShadeBlock = 256;
-constexpr int kWfStack = 16;    // LDS stack entries per lane in k_wf_trace
+constexpr int kWfStack = kStackLds;  // LDS stack entries per lane in k_wf_trace
 constexpr int kWfChunkMax = 1024;
 
 
@@ -240,7 +240,6 @@ k_wf_trace(DevScene sc, DevFrame fr, WfState st, unsigned long long* __restrict_
   __syncthreads();
   if (cnt == 0) return;
   int* lds = s_stack + lane;
-  int priv[kStackScratch];
   TravStats ts{0u, 0u, 0u, 0u};
   uint32_t next = 0;
   bool active = false;
@@ -265,7 +264,7 @@ k_wf_trace(DevScene sc, DevFrame fr, WfState st, unsigned long long* __restrict_
       next += n_idle;
     }
     if (!__any(active)) break;
-    if (active && trav_step<STATS, kWfStack>(sc, o, d, t, lds, priv, ts)) {
+    if (active && trav_step<STATS, kWfStack>(sc, o, d, t, lds, ts)) {
       st.res_i[slot] = t.found ? t.bi : kNoHit;
       st.res_t[slot] = t.bt;
       active = false;
