@@ -30,8 +30,12 @@ for cfg in configs:
     os.environ.clear()
     os.environ.update(base_env)
     os.environ.update(cfg)
-    r = ctx.render_tile(cam, W, H, want=("u8",), stats=True)
+    reps = int(os.environ.get("REPS", "1"))  # min over reps (single frames vary ~2%)
+    runs = [ctx.render_tile(cam, W, H, want=("u8",), stats=(i == 0)) for i in range(reps)]
+    r = runs[0]
     st = r["stats"]
+    st["kernel_ms"] = min([st["kernel_ms"]] + [ctx.render_tile(cam, W, H, want=(), stats=True)["stats"]["kernel_ms"]
+                                                 for _ in range(reps - 1)])
     same = ref is None or np.array_equal(r["u8"], ref)
     ref = r["u8"] if ref is None else ref
     print(json.dumps({**cfg, "ms": round(st["kernel_ms"], 2), "trace_ms": round(st["trace_ms"], 2),

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "libwgt.so")
+LIB_PATH = os.environ.get("WGT_LIB_PATH") or os.path.join(PKG_DIR, "libwgt.so")  # override: A/B runs
 
 # Byte layouts of include/wgt_api.h (= the reference GPU buffers)
 QUAD_DTYPE = np.dtype([("pos", "<f4", 4), ("right", "<f4", 4), ("up", "<f4", 4), ("norm", "<f4", 4),

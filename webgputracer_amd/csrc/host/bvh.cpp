@@ -234,14 +234,16 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, Bv
   out.n_nodes = (uint32_t)(out.nodes.size() / 16);
   const double ra = root_box.area();
   if (ra > 0) out.sah_cost /= ra;
-  out.tris.resize((size_t)n * 12);
+  out.tris.resize((size_t)n * kTriRecordFloats);
   for (uint32_t i = 0; i < n; ++i) {
     const wgt_triangle& t = tris[prims[i].idx];
-    float* o = &out.tris[(size_t)i * 12];
+    const Box& b = prims[i].b;
+    float* o = &out.tris[(size_t)i * kTriRecordFloats];
     o[0] = t.v0[0]; o[1] = t.v0[1]; o[2] = t.v0[2];
     std::memcpy(&o[3], &prims[i].idx, 4);
-    o[4] = t.e1[0]; o[5] = t.e1[1]; o[6] = t.e1[2]; o[7] = 0.0f;
-    o[8] = t.e2[0]; o[9] = t.e2[1]; o[10] = t.e2[2]; o[11] = 0.0f;
+    o[4] = t.e1[0]; o[5] = t.e1[1]; o[6] = t.e1[2]; o[7] = b.lo[0];
+    o[8] = t.e2[0]; o[9] = t.e2[1]; o[10] = t.e2[2]; o[11] = b.lo[1];
+    o[12] = b.lo[2]; o[13] = b.hi[0]; o[14] = b.hi[1]; o[15] = b.hi[2];
   }
   out.tshade.resize((size_t)n * 8);
   for (uint32_t i = 0; i < n; ++i) {

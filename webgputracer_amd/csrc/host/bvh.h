@@ -13,7 +13,7 @@ namespace wgt {
 
 struct BvhOut {
   std::vector<float> nodes;   // 16 floats per node (4 x float4)
-  std::vector<float> tris;    // 12 floats per triangle, leaf order, v0.w = orig index bits
+  std::vector<float> tris;    // kTriRecordFloats per triangle, leaf order (wgt_geom.h)
   std::vector<float> tshade;  // 8 floats per original triangle
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;
   double sah_cost = 0.0;

@@ -179,23 +179,20 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
   bool pop;
   int next = 0;
   if (t.lf < t.le) {
-    const float4* __restrict__ tp = sc.tris + 3 * t.lf;
+    const float4* __restrict__ tp = sc.tris + 4 * t.lf;
     const float4 A = tp[0], B = tp[1], C = tp[2];
     if (STATS) st.tris++;
-    const f3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
     float tt;
-    if (mt_test(o, d, v0, e1, e2, tt)) {
-      const uint32_t idx = __float_as_uint(A.w);
-      if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
-        f3 lo, hi;
-        tri_box(v0, e1, e2, lo, hi);
-        float bn, bf;
-        slab(t.ot, t.inv, lo, hi, bn, bf);
-        if (bn <= tt && tt <= bf) {
-          t.bt = tt;
-          t.bi = idx;
-          t.found = true;
-        }
+    const bool mt = mt_test(o, d, xyz(A), xyz(B), xyz(C), tt);
+    const uint32_t idx = __float_as_uint(A.w);
+    if (mt & ((tt < t.bt) | ((tt == t.bt) & (idx < t.bi)))) {
+      const float4 D = tp[3];
+      float bn, bf;
+      slab(t.ot, t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
+      if (bn <= tt && tt <= bf) {
+        t.bt = tt;
+        t.bi = idx;
+        t.found = true;
       }
     }
     ++t.lf;

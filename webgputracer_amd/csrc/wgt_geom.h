@@ -61,7 +61,8 @@ WGT_HD void slab(f3 ot, f3 inv, f3 lo, f3 hi, float& tnear, float& tfar) {
 }
 WGT_HD f3 slab_offset(f3 o, f3 inv) { return f3{-(o.x * inv.x), -(o.y * inv.y), -(o.z * inv.z)}; }
 
-// Two-sided Moller-Trumbore (fixed op order).
+// Two-sided Moller-Trumbore (fixed op order).  The early-outs
+// stay: a branch-free form (one combined predicate) measured slower on sponza.
 WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {
   f3 pvec = cross(d, e2);
   float det = dot(e1, pvec);
@@ -78,6 +79,14 @@ WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {
   tout = t;
   return true;
 }
+
+// Leaf-ordered triangle record, 64 B (4 x float4), one cache-line half:
+//   A = (v0.xyz, original index bits)   B = (e1.xyz, box.lo.x)
+//   C = (e2.xyz, box.lo.y)              D = (box.lo.z, box.hi.xyz)
+// A-C feed Moller-Trumbore; D (same 128-B line) is read only for a candidate
+// closest hit, to check t against the triangle's own padded box (tri_box,
+// computed by the host builder with the same fp32 operations).
+constexpr int kTriRecordFloats = 16;
 
 // BVH2 node, 64 B (4 x float4):
 //   a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
