@@ -121,9 +121,12 @@ typedef struct {
 
 typedef struct {
   uint32_t n_lights, n_quads, n_spheres, n_tris;
-  uint32_t bvh_nodes, bvh_leaves, bvh_max_depth, bvh_max_leaf;
+  uint32_t bvh_nodes, bvh_leaves, bvh_max_depth, bvh_max_leaf; /* the traversed (BVH4) tree */
   uint64_t device_bytes; /* scene bytes resident in HBM */
-  double sah_cost;
+  double sah_cost;       /* of the SAH BVH2 the BVH4 is collapsed from */
+  uint32_t bvh_width;    /* children per node (4) */
+  uint32_t bvh_stack;    /* worst-case traversal stack entries per ray (LDS) */
+  uint32_t bvh2_nodes, bvh2_depth;
 } wgt_scene_info;
 
 typedef struct wgt_ctx wgt_ctx;
@@ -144,6 +147,13 @@ int wgt_upload_scene(wgt_ctx *ctx, const wgt_quad *lights, uint32_t n_lights,
                      const wgt_quad *quads, uint32_t n_quads, const wgt_sphere *spheres,
                      uint32_t n_spheres, const wgt_triangle *tris, uint32_t n_tris);
 int wgt_scene_info_get(const wgt_ctx *ctx, wgt_scene_info *info);
+/* Host only (no device): build the BVH exactly as wgt_upload_scene does and
+ * export it for inspection.  info gets the counts; nodes_out (may be NULL) gets
+ * bvh_nodes x 32 floats (BVH4 layout, wgt_geom.h) if nodes_cap >= bvh_nodes;
+ * tris_out (may be NULL) gets n_tris x 16 floats (leaf-ordered records).
+ * Call once with NULL outputs to size them. */
+int wgt_bvh_build(const wgt_triangle *tris, uint32_t n_tris, float *nodes_out, uint32_t nodes_cap,
+                  float *tris_out, wgt_scene_info *info);
 
 /* ---- rendering (replaces the compute pass of Renderer::OnRender) --------- */
 /* Synchronous: render the rectangle [x0,x0+tw) x [y0,y0+th) of a W x H frame

@@ -15,6 +15,7 @@ W, H, spp = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 108
 ctx = w.Context(0)
 ctx.upload_scene(*w.mesh_scene(scene))
 cam = w.camera_param(W / H, spp, 0)
+print(json.dumps(ctx.scene_info()), flush=True)
 ref = None
 configs = [{"WGT_KERNEL": "1"}, {"WGT_KERNEL": "2"}]
 for rays in ("1", "2", "4", "8"):
@@ -30,12 +31,10 @@ for cfg in configs:
     os.environ.clear()
     os.environ.update(base_env)
     os.environ.update(cfg)
-    reps = int(os.environ.get("REPS", "1"))  # min over reps (single frames vary ~2%)
-    runs = [ctx.render_tile(cam, W, H, want=("u8",), stats=(i == 0)) for i in range(reps)]
-    r = runs[0]
+    r = ctx.render_tile(cam, W, H, want=("u8",), stats=True)
     st = r["stats"]
-    st["kernel_ms"] = min([st["kernel_ms"]] + [ctx.render_tile(cam, W, H, want=(), stats=True)["stats"]["kernel_ms"]
-                                                 for _ in range(reps - 1)])
+    for _ in range(int(os.environ.get("REPS", "1")) - 1):  # min over reps (single frames vary ~2%)
+        st["kernel_ms"] = min(st["kernel_ms"], ctx.render_tile(cam, W, H, want=("u8",), stats=True)["stats"]["kernel_ms"])
     same = ref is None or np.array_equal(r["u8"], ref)
     ref = r["u8"] if ref is None else ref
     print(json.dumps({**cfg, "ms": round(st["kernel_ms"], 2), "trace_ms": round(st["trace_ms"], 2),
@@ -44,5 +43,9 @@ for cfg in configs:
                       "svc_util": round(st["loop_lane_iters"] / max(64 * st["loop_wave_iters"], 1), 3),
                       "trav_util": round(st["trav_lane_steps"] / max(64 * st["trav_wave_steps"], 1), 3),
                       "svc_frac": round(st["cyc_service"] / max(st["cyc_service"] + st["cyc_trav"], 1), 3),
+                      "svc_cyc_per_iter": round(st["cyc_service"] / max(st["loop_wave_iters"], 1), 1),
+                      "trav_cyc_per_step": round(st["cyc_trav"] / max(st["trav_wave_steps"], 1), 1),
+                      "wave_iters": st["loop_wave_iters"], "wave_steps": st["trav_wave_steps"],
+                      "nodes": st["node_visits"], "tris": st["tri_tests"], "rays": st["traced_rays"],
                       "identical": bool(same)}), flush=True)
 ctx.close()

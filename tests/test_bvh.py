@@ -1,0 +1,125 @@
+"""Host BVH builder invariants (CPU only, through the C-ABI wgt_bvh_build).
+
+The kernels' traversal is exact (returns the brute-force closest triangle of the
+geometry spec) only if the exported tree satisfies:
+  * every triangle appears in exactly one leaf, leaves hold <= 8 triangles;
+  * every child box contains, bit for bit, the padded boxes of all triangles
+    below it (the slab test is then conservative: rounding is monotone);
+  * the per-triangle padded box stored in the record equals tri_box of the spec;
+  * the LDS stack (DevScene::stack entries) is >= the worst-case push depth.
+These are checked here against an independent numpy walk of the exported nodes.
+"""
+import numpy as np
+import pytest
+
+import webgputracer_amd as w
+
+f32 = np.float32
+STACK_MAX = 36  # kStackMax (wgt_internal.h)
+EMPTY = f32(3e38)  # kEmptySlotCoord (wgt_geom.h)
+
+
+def tri_box_np(v0, e1, e2):
+    """tri_box (wgt_geom.h) restated in numpy fp32: bounds of v0, v0+e1, v0+e2 padded by
+    ((hi-lo)*1e-4 + (|lo|+|hi|)*1e-5) + 1e-6 per axis."""
+    a, b, d = v0, v0 + e1, v0 + e2
+    mn = np.where(a < b, a, b)
+    mn = np.where(mn < d, mn, d)
+    mx = np.where(a > b, a, b)
+    mx = np.where(mx > d, mx, d)
+    pad = ((mx - mn) * f32(1e-4) + (np.abs(mn) + np.abs(mx)) * f32(1e-5)) + f32(1e-6)
+    return mn - pad, mx + pad
+
+
+def random_soup(n, seed, spread=500.0, size=20.0):
+    rng = np.random.default_rng(seed)
+    v0 = rng.uniform(0, spread, (n, 3)).astype(f32)
+    v = np.stack([v0, v0 + rng.normal(0, size, (n, 3)).astype(f32), v0 + rng.normal(0, size, (n, 3)).astype(f32)], 1)
+    return w.make_triangles(v)
+
+
+def check_tree(tris):
+    info, nodes, recs = w.bvh_build(tris)
+    n = len(tris)
+    assert info["bvh_width"] == 4
+    assert info["bvh_max_leaf"] <= 8
+    assert 1 <= info["bvh_stack"] <= STACK_MAX
+    assert info["bvh2_depth"] <= 24
+
+    # records: v0/e1/e2 of the original triangle, index bits, padded box == spec
+    idx = recs[:, 0, 3].view(np.uint32)
+    assert sorted(idx.tolist()) == list(range(n))
+    v0, e1, e2 = recs[:, 0, :3], recs[:, 1, :3], recs[:, 2, :3]
+    np.testing.assert_array_equal(v0, tris["v0"][idx][:, :3])
+    np.testing.assert_array_equal(e1, tris["e1"][idx][:, :3])
+    np.testing.assert_array_equal(e2, tris["e2"][idx][:, :3])
+    lo = np.stack([recs[:, 1, 3], recs[:, 2, 3], recs[:, 3, 0]], 1)
+    hi = recs[:, 3, 1:4]
+    elo, ehi = tri_box_np(v0, e1, e2)
+    np.testing.assert_array_equal(lo, elo)
+    np.testing.assert_array_equal(hi, ehi)
+
+    # walk: child boxes contain their subtree's triangle boxes; leaves partition the triangles
+    seen = np.zeros(n, np.int32)
+    refs = nodes[:, 6, :].view(np.int32)
+
+    def walk(node):
+        """-> (lo, hi, stack_need) of the subtree under BVH4 node `node`."""
+        sub_lo, sub_hi = np.full(3, np.inf, f32), np.full(3, -np.inf, f32)
+        need_children, live = 0, 0
+        for s in range(4):
+            box_lo = nodes[node, [0, 2, 4], s]
+            box_hi = nodes[node, [1, 3, 5], s]
+            if (box_lo == EMPTY).all():  # empty slot: far point box, never entered
+                assert (box_hi == EMPTY).all()
+                continue
+            live += 1
+            r = int(refs[node, s])
+            if r >= 0:
+                assert r > node  # preorder: children after the parent
+                clo, chi, need = walk(r)
+                need_children = max(need_children, need)
+            else:
+                u = (~r) & 0xFFFFFFFF
+                first, count = u >> 3, (u & 7) + 1
+                seen[first:first + count] += 1
+                clo, chi = lo[first:first + count].min(0), hi[first:first + count].max(0)
+            assert (box_lo <= clo).all() and (box_hi >= chi).all(), f"node {node} slot {s} does not contain its subtree"
+            sub_lo, sub_hi = np.minimum(sub_lo, box_lo), np.maximum(sub_hi, box_hi)
+        assert live >= 1
+        return sub_lo, sub_hi, (live - 1) + need_children
+
+    import sys
+    old = sys.getrecursionlimit()
+    sys.setrecursionlimit(max(old, 10000))
+    try:
+        _, _, need = walk(0)
+    finally:
+        sys.setrecursionlimit(old)
+    assert (seen == 1).all(), "every triangle in exactly one leaf"
+    assert max(need, 1) == info["bvh_stack"], (need, info["bvh_stack"])  # >= 1 entry allocated
+    return info
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (2, 1), (7, 2), (9, 3), (1000, 4), (5000, 5)])
+def test_bvh_random_soup(n, seed):
+    check_tree(random_soup(n, seed))
+
+
+def test_bvh_coincident_centroids():
+    # 300 copies of one triangle: no SAH split exists, median splits must still terminate
+    v = np.tile(np.array([[[0, 0, 0], [10, 0, 0], [0, 10, 0]]], f32), (300, 1, 1))
+    check_tree(w.make_triangles(v))
+
+
+def test_bvh_procedural_bunny():
+    info = check_tree(w.procedural_mesh("bunny", 20000))
+    assert info["bvh_max_depth"] < info["bvh2_depth"]  # the collapse shortens paths
+
+
+def test_bvh_full_size_meshes_stack_bound():
+    # the BASELINE mesh configs at full size: only the counts (the walk is the small cases' job)
+    for kind in ("bunny", "sponza"):
+        info, _, _ = w.bvh_build(w.procedural_mesh(kind))
+        assert 1 <= info["bvh_stack"] <= STACK_MAX
+        assert info["bvh2_depth"] <= 24 and info["bvh_max_leaf"] <= 8

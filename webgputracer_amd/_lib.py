@@ -47,7 +47,8 @@ class WgtSceneInfo(ctypes.Structure):
     _fields_ = [("n_lights", ctypes.c_uint32), ("n_quads", ctypes.c_uint32), ("n_spheres", ctypes.c_uint32),
                 ("n_tris", ctypes.c_uint32), ("bvh_nodes", ctypes.c_uint32), ("bvh_leaves", ctypes.c_uint32),
                 ("bvh_max_depth", ctypes.c_uint32), ("bvh_max_leaf", ctypes.c_uint32),
-                ("device_bytes", ctypes.c_uint64), ("sah_cost", ctypes.c_double)]
+                ("device_bytes", ctypes.c_uint64), ("sah_cost", ctypes.c_double), ("bvh_width", ctypes.c_uint32),
+                ("bvh_stack", ctypes.c_uint32), ("bvh2_nodes", ctypes.c_uint32), ("bvh2_depth", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -59,7 +60,7 @@ EXPORTS = [
     "wgt_upload_scene", "wgt_scene_info_get", "wgt_render_tile", "wgt_render_tiles_async",
     "wgt_render_tiles_stats", "wgt_render_tiles_profile", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_stream",
     "wgt_scene_cornell", "wgt_make_triangles", "wgt_load_obj", "wgt_procedural_mesh",
-    "wgt_write_obj", "wgt_write_png",
+    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build",
 ]
 
 _lib = None
@@ -102,8 +103,11 @@ def lib():
         "wgt_procedural_mesh": (I, [I, U32, U32, P, ctypes.POINTER(U32)]),
         "wgt_write_obj": (I, [ctypes.c_char_p, P, U32]),
         "wgt_write_png": (I, [ctypes.c_char_p, P, U32, U32]),
+        "wgt_bvh_build": (I, [P, U32, P, U32, P, ctypes.POINTER(WgtSceneInfo)]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("WGT_LIB_PATH") and not hasattr(L, name):
+            continue  # an older build loaded for same-box A/B timing
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

@@ -1,7 +1,9 @@
-// bvh.cpp — binned-SAH BVH2 builder.  Leaf boxes are unions of the padded
-// triangle boxes of the geometry spec (wgt_geom.h tri_box, evaluated on the host
-// with the same fp32 operations), so every node box contains, bit for bit, the
-// boxes of all triangles below it: the traversal is exact.
+// bvh.cpp — binned-SAH BVH2 builder, collapsed into the 4-wide BVH the kernels
+// traverse.  Leaf boxes are unions of the padded triangle boxes of the geometry
+// spec (wgt_geom.h tri_box, evaluated on the host with the same fp32 operations),
+// so every node box contains, bit for bit, the boxes of all triangles below it:
+// the traversal is exact.  The collapse only regroups BVH2 child
+// boxes, so the BVH4 child boxes are exactly BVH2 node boxes.
 #include "bvh.h"
 
 #include <algorithm>
@@ -57,7 +59,8 @@ constexpr double kCostTri = 1.0;
 
 class Builder {
  public:
-  Builder(std::vector<Prim>& p, BvhOut& o, uint32_t limit) : prims_(p), out_(o), limit_(limit) {}
+  Builder(std::vector<Prim>& p, BvhOut& o, std::vector<float>& n2, uint32_t limit)
+      : prims_(p), out_(o), nodes_(n2), limit_(limit) {}
 
   // Returns the child reference of the subtree over prims_[begin, end).
   int Build(uint32_t begin, uint32_t end, uint32_t depth, Box& box) {
@@ -72,7 +75,7 @@ class Builder {
       }
     }
     const uint32_t count = end - begin;
-    out_.max_depth = std::max(out_.max_depth, depth);
+    out_.depth2 = std::max(out_.depth2, depth);
     if (count == 1) return MakeLeaf(begin, count, box);
 
     uint32_t mid = begin;
@@ -150,8 +153,8 @@ class Builder {
                          return a.c[axis] < b.c[axis] || (a.c[axis] == b.c[axis] && a.idx < b.idx);
                        });
     }
-    const uint32_t id = (uint32_t)(out_.nodes.size() / 16);
-    out_.nodes.resize(out_.nodes.size() + 16);
+    const uint32_t id = (uint32_t)(nodes_.size() / 16);
+    nodes_.resize(nodes_.size() + 16);
     Box bl, br;
     const int rl = Build(begin, mid, depth + 1, bl);
     const int rr = Build(mid, end, depth + 1, br);
@@ -161,7 +164,7 @@ class Builder {
   }
 
   void WriteNode(uint32_t id, const Box& b0, int r0, const Box& b1, int r1) {
-    float* n = &out_.nodes[(size_t)id * 16];
+    float* n = &nodes_[(size_t)id * 16];
     n[0] = b0.lo[0]; n[1] = b0.hi[0]; n[2] = b0.lo[1]; n[3] = b0.hi[1];
     n[4] = b1.lo[0]; n[5] = b1.hi[0]; n[6] = b1.lo[1]; n[7] = b1.hi[1];
     n[8] = b0.lo[2]; n[9] = b0.hi[2]; n[10] = b1.lo[2]; n[11] = b1.hi[2];
@@ -181,13 +184,97 @@ class Builder {
 
   std::vector<Prim>& prims_;
   BvhOut& out_;
+  std::vector<float>& nodes_;
   uint32_t limit_;
+};
+
+
+// BVH2 child `which` (0/1) of node `id`, from the 16-float BVH2 layout.
+struct Child {
+  Box b;
+  int ref;
+};
+Child Child2(const std::vector<float>& n2, int id, int which) {
+  const float* n = &n2[(size_t)id * 16];
+  Child c;
+  const int o = which ? 4 : 0;
+  c.b.lo[0] = n[o + 0]; c.b.hi[0] = n[o + 1]; c.b.lo[1] = n[o + 2]; c.b.hi[1] = n[o + 3];
+  c.b.lo[2] = n[8 + 2 * which]; c.b.hi[2] = n[9 + 2 * which];
+  std::memcpy(&c.ref, &n[12 + which], 4);
+  return c;
+}
+
+// Greedy collapse: a BVH4 node starts from the two children of a BVH2 node and
+// repeatedly opens its largest-area internal child until it has 4 slots.  Returns
+// the BVH4 node index; `need` receives the worst-case stack entries of the
+// subtree: the traversal pushes at most (children - 1) per node on a root-to-node
+// path, so need = (children - 1) + max over internal children.
+class Collapser {
+ public:
+  // pairs = true: open only the BVH2 node's own two children (a BVH4 node = two
+  // BVH2 levels), so BVH4 depth <= ceil(BVH2 depth / 2): the bounded fallback.
+  Collapser(const std::vector<float>& n2, BvhOut& o, bool pairs) : n2_(n2), out_(o), pairs_(pairs) {}
+
+  int Collapse(int id2, uint32_t depth, uint32_t& need) {
+    Child ch[kBvhWidth];
+    int n = 2;
+    ch[0] = Child2(n2_, id2, 0);
+    ch[1] = Child2(n2_, id2, 1);
+    const int orig = n;
+    bool opened[2] = {false, false};  // pairs mode: each original child opens once
+    while (n < kBvhWidth) {
+      int best = -1;
+      double ba = -1.0;
+      for (int i = 0; i < (pairs_ ? orig : n); ++i)
+        if (ch[i].ref >= 0 && ch[i].b.area() > ba && !(pairs_ && opened[i])) {
+          ba = ch[i].b.area();
+          best = i;
+        }
+      if (best < 0) break;
+      const int r = ch[best].ref;
+      ch[best] = Child2(n2_, r, 0);
+      ch[n++] = Child2(n2_, r, 1);
+      if (best < 2) opened[best] = true;
+    }
+    const uint32_t id = (uint32_t)(out_.nodes.size() / kNode4Floats);
+    out_.nodes.resize(out_.nodes.size() + kNode4Floats);
+    out_.max_depth = std::max(out_.max_depth, depth + 1);
+    int refs[kBvhWidth];
+    uint32_t sub = 0;
+    for (int i = 0; i < n; ++i) {
+      if (ch[i].ref >= 0) {
+        uint32_t s = 0;
+        refs[i] = Collapse(ch[i].ref, depth + 1, s);
+        sub = std::max(sub, s);
+      } else {
+        refs[i] = ch[i].ref;
+      }
+    }
+    need = (uint32_t)(n - 1) + sub;
+    float* o = &out_.nodes[(size_t)id * kNode4Floats];
+    for (int i = 0; i < kBvhWidth; ++i) {
+      const bool live = i < n;
+      for (int c = 0; c < 3; ++c) {
+        o[(2 * c) * 4 + i] = live ? ch[i].b.lo[c] : kEmptySlotCoord;
+        o[(2 * c + 1) * 4 + i] = live ? ch[i].b.hi[c] : kEmptySlotCoord;
+      }
+      const int r = live ? refs[i] : refs[0];
+      std::memcpy(&o[24 + i], &r, 4);
+      o[28 + i] = 0.0f;
+    }
+    return (int)id;
+  }
+
+ private:
+  const std::vector<float>& n2_;
+  BvhOut& out_;
+  bool pairs_;
 };
 
 }  // namespace
 
-bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, BvhOut& out,
-              std::string& err) {
+bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
+              BvhOut& out, std::string& err) {
   out = BvhOut{};
   if (n == 0) { err = "BuildBvh: no triangles"; return false; }
   if (n >= (1u << 28)) { err = "BuildBvh: too many triangles (max 2^28-1)"; return false; }
@@ -209,31 +296,45 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, Bv
       }
     }
   }
-  out.nodes.reserve((size_t)16 * 2 * (n / 2 + 1));
   if (MedianDepth(n) > max_depth_limit) {
     err = "BuildBvh: too many triangles for depth limit " + std::to_string(max_depth_limit);
     return false;
   }
-  Builder b(prims, out, max_depth_limit);
+  std::vector<float> n2;
+  n2.reserve((size_t)16 * 2 * (n / 2 + 1));
+  Builder b(prims, out, n2, max_depth_limit);
   Box root_box;
   const int root = b.Build(0, n, 0, root_box);
   if (root < 0) {
-    // single leaf: a root node whose second child can never be hit (NaN box:
-    // every slab comparison is false).
-    out.nodes.assign(16, 0.0f);
-    Box nanbox;
-    for (int c = 0; c < 3; ++c) nanbox.lo[c] = nanbox.hi[c] = std::numeric_limits<float>::quiet_NaN();
-    b.WriteNode(0, root_box, root, nanbox, root);
-    out.max_depth = 1;
+    // single leaf: a root node whose second child is an empty slot (wgt_geom.h)
+    n2.assign(16, 0.0f);
+    Box empty;
+    for (int c = 0; c < 3; ++c) empty.lo[c] = empty.hi[c] = kEmptySlotCoord;
+    b.WriteNode(0, root_box, root, empty, root);
+    out.depth2 = 1;
   }
-  if (out.max_depth > max_depth_limit) {
-    err = "BuildBvh: depth " + std::to_string(out.max_depth) + " exceeds " +
-          std::to_string(max_depth_limit);
+  if (out.depth2 > max_depth_limit) {
+    err = "BuildBvh: depth " + std::to_string(out.depth2) + " exceeds " + std::to_string(max_depth_limit);
     return false;
   }
-  out.n_nodes = (uint32_t)(out.nodes.size() / 16);
+  out.n_nodes2 = (uint32_t)(n2.size() / 16);
   const double ra = root_box.area();
   if (ra > 0) out.sah_cost /= ra;
+  out.nodes.reserve(n2.size() * 2);
+  Collapser greedy(n2, out, false);
+  greedy.Collapse(0, 0, out.stack_need);
+  if (out.stack_need > stack_limit) {
+    out.nodes.clear();
+    out.max_depth = 0;
+    Collapser pairs(n2, out, true);
+    pairs.Collapse(0, 0, out.stack_need);
+  }
+  if (out.stack_need > stack_limit) {
+    err = "BuildBvh: traversal stack " + std::to_string(out.stack_need) + " exceeds " +
+          std::to_string(stack_limit);
+    return false;
+  }
+  out.n_nodes = (uint32_t)(out.nodes.size() / kNode4Floats);
   out.tris.resize((size_t)n * kTriRecordFloats);
   for (uint32_t i = 0; i < n; ++i) {
     const wgt_triangle& t = tris[prims[i].idx];

@@ -12,16 +12,20 @@
 namespace wgt {
 
 struct BvhOut {
-  std::vector<float> nodes;   // 16 floats per node (4 x float4)
+  std::vector<float> nodes;   // kNode4Floats per BVH4 node (wgt_geom.h layout), root = 0
   std::vector<float> tris;    // kTriRecordFloats per triangle, leaf order (wgt_geom.h)
   std::vector<float> tshade;  // 8 floats per original triangle
-  uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;
+  uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;  // BVH4 nodes / depth
+  uint32_t n_nodes2 = 0, depth2 = 0;  // the SAH BVH2 the BVH4 was collapsed from
+  uint32_t stack_need = 0;            // worst-case traversal stack entries (exact for this tree)
   double sah_cost = 0.0;
 };
 
-// Builds over n >= 1 triangles.  max_depth_limit bounds the tree depth (the
-// traversal stack holds at most depth entries).
-bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, BvhOut& out,
-              std::string& err);
+// Builds over n >= 1 triangles.  max_depth_limit bounds the BVH2 depth, which
+// bounds the BVH4 depth and so the traversal stack (stack_need <= 3 * depth).
+// stack_limit bounds stack_need: a greedy collapse over the limit is redone
+// two-levels-per-node (stack_need <= 3 * ceil(depth2 / 2)).
+bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
+              BvhOut& out, std::string& err);
 
 }  // namespace wgt

@@ -137,9 +137,9 @@ __device__ __forceinline__ void simt_count(uint32_t& wave, uint32_t& lane) {
   ++lane;
 }
 
-// Resumable BVH2 traversal: closest triangle = min (t, index) with t < bound (or
-// t <= bound and index < bi when bi = kNoHit).  Per-lane stack: kStackLds entries
-// in LDS (stride kBlock, conflict-free).
+// Resumable BVH4 traversal: closest triangle = min (t, index) with t < bound (or
+// t <= bound and index < bi when bi = kNoHit).  Per-lane stack: DevScene::stack
+// entries in LDS (stride kBlock, conflict-free).
 struct Trav {
   f3 inv, ot;
   float bt;
@@ -165,14 +165,44 @@ __device__ __forceinline__ void trav_init(f3 o, f3 d, bool quad_hit, float qt, T
 }
 
 
-// One BVH node OR one triangle per call (a leaf is opened as a range and its
+// Sort key of one BVH4 child: the clamped entry distance max(near, kRayMin)
+// (positive, so its bits order as unsigned) with the slot in the low 2 bits;
+// kMissKey if the ray misses the box or the box lies beyond the current closest
+// hit.  hit = max(near, kRayMin) <= min(far, bt) is the node test
+// near <= far && near <= bt && far >= kRayMin, because bt >= kRayMin always
+// (bt is kRayMax, a quad t or a triangle t, all >= kRayMin).
+constexpr uint32_t kMissKey = 0xFFFFFFFFu;
+__device__ __forceinline__ uint32_t child_key(const Trav& t, float lx, float hx, float ly, float hy,
+                                              float lz, float hz, uint32_t slot) {
+  const float t0x = __builtin_fmaf(lx, t.inv.x, t.ot.x), t1x = __builtin_fmaf(hx, t.inv.x, t.ot.x);
+  const float t0y = __builtin_fmaf(ly, t.inv.y, t.ot.y), t1y = __builtin_fmaf(hy, t.inv.y, t.ot.y);
+  const float t0z = __builtin_fmaf(lz, t.inv.z, t.ot.z), t1z = __builtin_fmaf(hz, t.inv.z, t.ot.z);
+  const float n = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t0x, t1x), __builtin_fminf(t0y, t1y)),
+                                  __builtin_fmaxf(__builtin_fminf(t0z, t1z), kRayMin));
+  const float f = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
+                                  __builtin_fminf(__builtin_fmaxf(t0z, t1z), t.bt));
+  return n <= f ? ((__float_as_uint(n) & ~3u) | slot) : kMissKey;
+}
+// Compare-exchange of (key, ref) pairs: the smaller key (and its ref) to a.
+__device__ __forceinline__ void cas(uint32_t& ka, int& ra, uint32_t& kb, int& rb) {
+  const bool sw = kb < ka;
+  const uint32_t k = sw ? kb : ka;
+  kb = sw ? ka : kb;
+  ka = k;
+  const int r = sw ? rb : ra;
+  rb = sw ? ra : rb;
+  ra = r;
+}
+
+// One BVH4 node OR one triangle per call (a leaf is opened as a range and its
 // triangles are tested one per step), so every lane's step costs about the same
-// and a wave never pays for an 8-triangle leaf loop at every step.  The stack
-// lives in LDS only: the builder bounds the BVH depth by STACK (kMaxBvhDepth), so
-// it cannot overflow.  Push / pop / descend are written as selects around one
-// leaf-or-node branch to keep the exec-mask bookkeeping small.  Returns true when
-// the traversal has finished.
-template <bool STATS, int STACK = kStackLds>
+// and a wave never pays for an 8-triangle leaf loop at every step.  A node step
+// sorts its hit children by entry distance (5 compare-exchanges of (key, ref)), descends into
+// the nearest and pushes the others farthest first.  The stack lives in LDS
+// only, sized to the builder's exact worst case, so it cannot overflow.  Push /
+// pop / descend are selects around one leaf-or-node branch to keep the
+// exec-mask bookkeeping small.  Returns true when the traversal has finished.
+template <bool STATS>
 __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& t,
                                           int* __restrict__ lds, TravStats& st) {
   if (STATS) simt_count(st.wave_steps, st.lane_steps);
@@ -183,37 +213,48 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
     const float4 A = tp[0], B = tp[1], C = tp[2];
     if (STATS) st.tris++;
     float tt;
-    const bool mt = mt_test(o, d, xyz(A), xyz(B), xyz(C), tt);
-    const uint32_t idx = __float_as_uint(A.w);
-    if (mt & ((tt < t.bt) | ((tt == t.bt) & (idx < t.bi)))) {
-      const float4 D = tp[3];
-      float bn, bf;
-      slab(t.ot, t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
-      if (bn <= tt && tt <= bf) {
-        t.bt = tt;
-        t.bi = idx;
-        t.found = true;
+    if (mt_test(o, d, xyz(A), xyz(B), xyz(C), tt)) {
+      const uint32_t idx = __float_as_uint(A.w);
+      if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
+        const float4 D = tp[3];
+        float bn, bf;
+        slab(t.ot, t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
+        if (bn <= tt && tt <= bf) {
+          t.bt = tt;
+          t.bi = idx;
+          t.found = true;
+        }
       }
     }
     ++t.lf;
     if (t.lf < t.le) return false;
     pop = true;
   } else {
-    const float4* __restrict__ n = sc.nodes + 4 * t.ref;
-    const float4 a = n[0], b = n[1], c = n[2], e = n[3];
+    const float4* __restrict__ n = sc.nodes + 8 * t.ref;
+    const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
+    const float4 rf = n[6];
     if (STATS) st.nodes++;
-    float n0, f0, n1, f1;
-    slab(t.ot, t.inv, f3{a.x, a.z, c.x}, f3{a.y, a.w, c.y}, n0, f0);
-    slab(t.ot, t.inv, f3{b.x, b.z, c.z}, f3{b.y, b.w, c.w}, n1, f1);
-    const bool h0 = (n0 <= f0) & (n0 <= t.bt) & (f0 >= kRayMin);
-    const bool h1 = (n1 <= f1) & (n1 <= t.bt) & (f1 >= kRayMin);
-    const int r0 = __float_as_int(e.x), r1 = __float_as_int(e.y);
-    const bool both = h0 & h1;
-    const bool first1 = both ? (n1 < n0) : h1;  // descend into child 1
-    next = first1 ? r1 : r0;
-    if (both) lds[t.sp * kBlock] = first1 ? r0 : r1;
-    t.sp += both ? 1 : 0;
-    pop = !(h0 | h1);
+    int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z),
+        r3 = __float_as_int(rf.w);
+    uint32_t k0 = child_key(t, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, 0u);
+    uint32_t k1 = child_key(t, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, 1u);
+    uint32_t k2 = child_key(t, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, 2u);
+    uint32_t k3 = child_key(t, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, 3u);
+    cas(k0, r0, k1, r1);
+    cas(k2, r2, k3, r3);
+    cas(k0, r0, k2, r2);
+    cas(k1, r1, k3, r3);
+    cas(k1, r1, k2, r2);
+    // push the hit children other than the nearest, farthest first; a write for a
+    // missed child lands above the top and is overwritten or never read
+    lds[t.sp * kBlock] = r3;
+    t.sp += k3 != kMissKey ? 1 : 0;
+    lds[t.sp * kBlock] = r2;
+    t.sp += k2 != kMissKey ? 1 : 0;
+    lds[t.sp * kBlock] = r1;
+    t.sp += k1 != kMissKey ? 1 : 0;
+    next = r0;
+    pop = k0 == kMissKey;
   }
   if (pop) {
     if (t.sp == 0 || ++t.iters > sc.max_iters) return true;
@@ -347,17 +388,21 @@ struct Pixel {
 
 struct Counters {
   uint32_t q, tr, nan, lw, ll;
+  uint32_t px;  // pixels finished by this lane
 };
 
-// Pixel of this lane, or false if the lane has none.
-__device__ __forceinline__ bool pixel_setup(const DevFrame& fr, const wgt_tile* __restrict__ tiles,
-                                            uint32_t& tile, uint32_t& lx, uint32_t& ly, Pixel& px) {
+// Pixel of pixel slot (block, lane) = (slot >> 6, slot & 63): block b covers an
+// 8x8 sub-block of tile b / (sub-blocks per tile).  false if the slot is outside
+// its tile or the frame (ragged tiles).
+__device__ __forceinline__ bool slot_setup(const DevFrame& fr, const wgt_tile* __restrict__ tiles,
+                                           uint32_t block, uint32_t lane, uint32_t& tile,
+                                           uint32_t& lx, uint32_t& ly, Pixel& px) {
   const uint32_t bx = (fr.tw + 7u) >> 3, by = (fr.th + 7u) >> 3;
   const uint32_t bpt = bx * by;
-  tile = blockIdx.x / bpt;
-  const uint32_t rem = blockIdx.x - tile * bpt;
-  lx = (rem % bx) * 8u + (threadIdx.x & 7u);
-  ly = (rem / bx) * 8u + (threadIdx.x >> 3);
+  tile = block / bpt;
+  const uint32_t rem = block - tile * bpt;
+  lx = (rem % bx) * 8u + (lane & 7u);
+  ly = (rem / bx) * 8u + (lane >> 3);
   if (tile >= fr.n_tiles || lx >= fr.tw || ly >= fr.th) return false;
   const wgt_tile td = tiles[tile];
   px.x = td.x0 + lx;
@@ -368,6 +413,12 @@ __device__ __forceinline__ bool pixel_setup(const DevFrame& fr, const wgt_tile* 
   px.col = f3{0.0f, 0.0f, 0.0f};
   px.hit0 = kNoHit;
   return true;
+}
+
+// Pixel of this lane in a one-pixel-per-lane launch, or false if the lane has none.
+__device__ __forceinline__ bool pixel_setup(const DevFrame& fr, const wgt_tile* __restrict__ tiles,
+                                            uint32_t& tile, uint32_t& lx, uint32_t& ly, Pixel& px) {
+  return slot_setup(fr, tiles, blockIdx.x, threadIdx.x, tile, lx, ly, px);
 }
 
 // setup_camera_ray + pixel_sample_square (path_tracer.wgsl:232-262) for sample px.k
@@ -417,13 +468,14 @@ __device__ __forceinline__ void write_pixel(const DevFrame& fr, uint32_t tile, u
 __device__ __forceinline__ void flush_counters(unsigned long long* __restrict__ counters,
                                                const Counters& c, const TravStats& st,
                                                uint32_t nsamp) {
+  // c.px pixels, nsamp samples each
   atomicAdd(&counters[CNT_QUERIES], (unsigned long long)c.q);
   atomicAdd(&counters[CNT_TRACED], (unsigned long long)c.tr);
-  atomicAdd(&counters[CNT_SAMPLES], (unsigned long long)nsamp);
+  atomicAdd(&counters[CNT_SAMPLES], (unsigned long long)nsamp * c.px);
   atomicAdd(&counters[CNT_NAN], (unsigned long long)c.nan);
   atomicAdd(&counters[CNT_NODES], (unsigned long long)st.nodes);
   atomicAdd(&counters[CNT_TRIS], (unsigned long long)st.tris);
-  atomicAdd(&counters[CNT_PIXELS], 1ull);
+  atomicAdd(&counters[CNT_PIXELS], (unsigned long long)c.px);
   atomicAdd(&counters[CNT_LOOP_WAVE], (unsigned long long)c.lw);
   atomicAdd(&counters[CNT_LOOP_LANE], (unsigned long long)c.ll);
   atomicAdd(&counters[CNT_TRAV_WAVE], (unsigned long long)st.wave_steps);

@@ -88,13 +88,20 @@ WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {
 // computed by the host builder with the same fp32 operations).
 constexpr int kTriRecordFloats = 16;
 
-// BVH2 node, 64 B (4 x float4):
-//   a = (c0.lo.x, c0.hi.x, c0.lo.y, c0.hi.y)
-//   b = (c1.lo.x, c1.hi.x, c1.lo.y, c1.hi.y)
-//   c = (c0.lo.z, c0.hi.z, c1.lo.z, c1.hi.z)
-//   d = (ref0, ref1, -, -) as int bits
+// BVH4 node, 128 B (8 x float4, one L2 cache line), children in SoA order:
+//   N[0] = lo.x of children 0..3   N[1] = hi.x   N[2] = lo.y   N[3] = hi.y
+//   N[4] = lo.z                    N[5] = hi.z   N[6] = child refs (int bits)
+//   N[7] = 0
+// An empty slot holds the point box at kEmptySlotCoord on every axis and a copy
+// of a live child's ref.  Its slab distances are beyond kRayMax (or negative) for
+// every ray with |d| < 1e18, so it is never entered; were it entered, the visit
+// would only repeat a live child: the closest hit never depends on culling beyond
+// its being conservative.
 // child ref >= 0: internal node index; < 0: leaf, ~ref = first*8 + (count-1)
 // into the leaf-ordered triangle array (count <= 8).
+constexpr int kBvhWidth = 4;
+constexpr float kEmptySlotCoord = 3e38f;
+constexpr int kNode4Floats = 32;
 constexpr int kLeafMax = 8;
 WGT_HD int leaf_ref(uint32_t first, uint32_t count) { return ~(int)(first * 8u + (count - 1u)); }
 WGT_HD uint32_t leaf_first(int ref) { return ((uint32_t)~ref) >> 3; }

@@ -5,9 +5,10 @@
 //   quads   : lights then quads, 96-B reference records (6 x float4) — read with
 //             wave-uniform (scalar) loads, 1.7 KB for the Cornell box
 //   spheres : 32-B reference records (2 x float4)
-//   nodes   : BVH2 nodes, 64 B (4 x float4), root = node 0, see wgt_geom.h
-//   tris    : leaf-ordered Moller-Trumbore records, 48 B (3 x float4):
-//             (v0.xyz, original index bits), (e1.xyz, 0), (e2.xyz, 0)
+//   nodes   : BVH4 nodes, 128 B (8 x float4, one cache line), root = node 0,
+//             see wgt_geom.h
+//   tris    : leaf-ordered Moller-Trumbore records, 64 B (4 x float4) carrying
+//             the padded triangle box, see wgt_geom.h
 //   tshade  : per ORIGINAL triangle, 32 B: (face_norm.xyz, emissive), (col.xyz, 0)
 #pragma once
 
@@ -19,11 +20,12 @@
 namespace wgt {
 
 constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
-// Per-lane traversal stack entries in LDS (6 KB per wave).  The BVH builder
-// guarantees depth <= kMaxBvhDepth, and the stack never holds more than the depth,
-// so the stack cannot overflow and needs no spill path.
-constexpr int kStackLds = 24;
-constexpr int kMaxBvhDepth = kStackLds;
+// Per-lane traversal stack in LDS, stride kBlock (conflict-free), sized per scene
+// at launch (dynamic LDS) to the builder's exact worst case DevScene::stack, so it
+// cannot overflow and needs no spill path.  kMaxBvhDepth bounds the SAH BVH2 the
+// BVH4 is collapsed from; kStackMax bounds the stack (9 KB per wave).
+constexpr int kMaxBvhDepth = 24;
+constexpr int kStackMax = 36;
 
 struct DevScene {
   const float4* __restrict__ quads;   // n_lights + n_quads records
@@ -35,8 +37,11 @@ struct DevScene {
   uint32_t n_nodes;
   uint32_t last_sphere_emissive;
   float light_area;  // length(cross(lights[0].right, lights[0].up)) (path_tracer.wgsl:205)
-  uint32_t max_iters; // traversal safety bound (2 x nodes + 2)
+  uint32_t max_iters; // traversal safety bound on pops (4 x nodes + 8)
+  uint32_t stack;     // traversal stack entries per lane (>= 1)
 };
+// Dynamic LDS bytes of a traversal kernel launch.
+inline size_t stack_lds_bytes(const DevScene& sc) { return (size_t)sc.stack * kBlock * sizeof(int); }
 
 // Per-frame camera constants of setup_camera_ray (path_tracer.wgsl:239-262),
 // computed once on the host with the same fp32 operations (wgt_math.h).
@@ -58,6 +63,13 @@ struct DevFrame {
   // wavefront: rays a slot may start per shade launch, slots per trace wave,
   // idle lanes that trigger a refill from the wave's ray list
   uint32_t wf_rays, wf_chunk, wf_refill;
+  // persistent k_render_ps: pixel slots of the launch (64 per 8x8 block), the
+  // idle lanes that trigger a refill from the pixel queue, LPT ordering on/off,
+  // the queue order (queue block q renders pixel block perm[q]; NULL = identity)
+  // and the pre-pass cost per pixel block (set by launch_render)
+  uint32_t n_slots, pq_refill, pq_lpt;
+  const uint32_t* perm;
+  uint32_t* cost;
 };
 
 // Wavefront path state, SoA over slots (one slot per pixel of the tile list).
@@ -104,9 +116,14 @@ enum {
 };
 
 // Launchers implemented in wgt_kernels.hip
+// k_render_ps runs persistent: at most `resident` waves (ps_resident_waves),
+// lanes pulling pixel slots from a per-launch queue in LPT order (1-spp cost
+// pre-pass + k_lpt_order), all stream-ordered on `stream`.
 hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
                          uchar4* out8, float4* out32, uint32_t* outhit,
-                         unsigned long long* counters, hipStream_t stream);
+                         unsigned long long* counters, uint32_t resident, hipStream_t stream);
+// Waves of k_render_ps resident on the whole device for this scene's LDS stack.
+hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves);
 hipError_t launch_trace(const DevScene& sc, const float* d_rays, uint32_t n, uint32_t* prim,
                         float* dist, hipStream_t stream);
 

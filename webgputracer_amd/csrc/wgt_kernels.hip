@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(kBlock)
 k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
          float4* __restrict__ out32, uint32_t* __restrict__ outhit,
          unsigned long long* __restrict__ counters) {
-  __shared__ int s_stack[kStackLds * kBlock];
+  extern __shared__ int s_stack[];  // sc.stack entries per lane (stack_lds_bytes)
   uint32_t tile, lx, ly;
   Pixel px;
   if (!pixel_setup(fr, tiles, tile, lx, ly, px)) return;
@@ -47,7 +47,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
   f3 ro{}, rd{}, pc{};
   int depth = 0;
   TravStats st{0u, 0u, 0u, 0u};
-  Counters c{0u, 0u, 0u, 0u, 0u};
+  Counters c{0u, 0u, 0u, 0u, 0u, 1u};  // one pixel per lane
 
   while (px.k < nsamp) {
     if (STATS) simt_count(c.lw, c.ll);
@@ -79,35 +79,89 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
   if (STATS) flush_counters(counters, c, st, nsamp);
 }
 
-// Phase-split kernel for scenes with triangles (see the file comment).
-template <bool STATS>
+// Phase-split kernel for scenes with triangles (see the file comment), persistent:
+// the grid is the resident wave capacity and lanes take pixels from the launch's
+// pixel queue (*queue counts handed-out pixel slots of 64 * blocks).  A lane
+// whose pixel has finished all its samples writes it and takes the next slot, so
+// no lane idles while its wave has work left and the launch has no tail of
+// late-started expensive tiles.  Queue block q is pixel block fr.perm[q] (LPT
+// order: most expensive first, from a COST pre-pass; see launch_render), so the
+// pixels still in flight when the queue drains are cheap ones; a wave's first 64
+// slots are one 8x8 pixel block.  Each pixel's result depends only on its
+// coordinates and seed: which lane or wave computes it does not change a bit.
+// COST: the 1-spp pre-pass: no output, each finished pixel adds its work units
+// (kCostService per ray started + 1 per traversal step) to fr.cost[its block].
+constexpr uint32_t kCostService = 7;  // a service iteration ~ 7 traversal steps (profiles/)
+template <bool STATS, bool COST>
 __global__ void __launch_bounds__(kBlock)
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
-            unsigned long long* __restrict__ counters) {
-  __shared__ int s_stack[kStackLds * kBlock];
-  uint32_t tile, lx, ly;
-  Pixel px;
-  if (!pixel_setup(fr, tiles, tile, lx, ly, px)) return;
+            unsigned long long* __restrict__ counters, uint32_t* __restrict__ queue) {
+  extern __shared__ int s_stack[];  // sc.stack entries per lane (stack_lds_bytes)
   int* lds = s_stack + threadIdx.x;
+  const uint32_t lane = threadIdx.x;
+  const unsigned long long lt_mask = (1ull << lane) - 1ull;
   const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
   const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
+  const uint32_t n_slots = fr.n_slots;
+  Pixel px{};
+  uint32_t tile = 0, lx = 0, ly = 0;
   f3 ro{}, rd{}, pc{};
   int depth = 0;
   TravStats st{0u, 0u, 0u, 0u};
-  Counters c{0u, 0u, 0u, 0u, 0u};
+  Counters c{0u, 0u, 0u, 0u, 0u, 0u};
   Trav t;
   uint32_t q_prim = kNoHit;  // quad part of the pending hit, rebuilt at finalisation
   float q_t = kRayMax;
-  bool done = nsamp == 0, trav = false, pending = false;
+  bool have = false;       // lane holds a pixel
+  bool exhausted = false;  // the queue is empty for this lane
+  bool trav = false, pending = false, fin = false;
   uint64_t cyc_svc = 0, cyc_trav = 0;
+  uint32_t pblock = 0, work = 0;  // COST: the pixel's block and its work so far
 
   for (;;) {
     // ------------------------------------------------------------ service phase
     uint64_t t_phase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
-      const bool need = !trav && !done;
-      if (!__any(need)) break;
+      if (fin) {  // a finished pixel: write it (here, outside the sample loop)
+        if (COST) {
+          atomicAdd(fr.cost + pblock, work);
+          work = 0;
+        } else {
+          write_pixel(fr, tile, lx, ly, px, out8, out32, outhit);
+        }
+        if (STATS) ++c.px;
+        fin = false;
+      }
+      // refill: lanes without a pixel take consecutive slots, one atomic per wave
+      const unsigned long long idle = __ballot(!have && !exhausted);
+      if (idle != 0ull) {
+        const uint32_t n_idle = (uint32_t)__popcll(idle);
+        if (n_idle >= fr.pq_refill || __ballot(have) == 0ull) {
+          const int leader = __ffsll((long long)idle) - 1;
+          uint32_t base = 0;
+          if ((int)lane == leader) base = atomicAdd(queue, n_idle);
+          base = __shfl(base, leader);
+          if (!have && !exhausted) {
+            const uint32_t slot = base + (uint32_t)__popcll(idle & lt_mask);
+            if (slot >= n_slots) {
+              exhausted = true;
+            } else {
+              const uint32_t b = fr.perm ? fr.perm[slot >> 6] : (slot >> 6);
+              if (slot_setup(fr, tiles, b, slot & 63u, tile, lx, ly, px)) {
+                have = true;
+                depth = 0;
+                pblock = b;
+              }
+            }
+          }
+        }
+      }
+      const bool need = have && !trav;
+      if (!__any(need)) {
+        if (__ballot(!have && !exhausted) != 0ull && __ballot(trav) == 0ull) continue;  // refill again
+        break;
+      }
       if (need) {
         if (STATS) simt_count(c.lw, c.ll);
         if (pending) {
@@ -128,7 +182,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
         // start the next ray of this pixel
         for (;;) {
           if (px.k >= nsamp) {
-            done = true;
+            have = false;
+            fin = true;
             break;
           }
           if (depth == 0) {
@@ -157,7 +212,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           quad_scan(sc, ro, rd, h, q_t);
           q_prim = h.prim;
           trav_init(ro, rd, q_prim != kNoHit, q_t, t);
-          // the root node is tested here: rays that miss both root children never
+          if (COST) work += kCostService;
+          // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
           if (trav_step<STATS>(sc, ro, rd, t, lds, st)) pending = true;
           else trav = true;
@@ -171,23 +227,23 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       cyc_svc += now - t_phase;
       t_phase = now;
     }
-    if (!__any(!done)) break;
+    if (__ballot(have || !exhausted) == 0ull) break;
     // --------------------------------------------------------- traversal phase
     for (;;) {
+      if (COST && trav) ++work;
       if (trav && trav_step<STATS>(sc, ro, rd, t, lds, st)) {
         trav = false;
         pending = true;
       }
       const uint32_t ntrav = (uint32_t)__popcll(__ballot(trav));
       if (ntrav == 0) break;
-      if (ntrav <= fr.ps_to_service && __any(!trav && !done)) break;
+      if (ntrav <= fr.ps_to_service && __any(!trav && (have || !exhausted))) break;
     }
     if (STATS) cyc_trav += __builtin_amdgcn_s_memtime() - t_phase;
   }
-  write_pixel(fr, tile, lx, ly, px, out8, out32, outhit);
   if (STATS) {
     flush_counters(counters, c, st, nsamp);
-    if (__lane_id() == (unsigned)(__ffsll((long long)__ballot(1)) - 1)) {
+    if (lane == 0) {
       atomicAdd(&counters[CNT_CYC_SERVICE], (unsigned long long)cyc_svc);
       atomicAdd(&counters[CNT_CYC_TRAV], (unsigned long long)cyc_trav);
     }
@@ -198,7 +254,7 @@ template <bool TRIS>
 __global__ void __launch_bounds__(kBlock)
 k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __restrict__ prim,
         float* __restrict__ dist) {
-  __shared__ int s_stack[kStackLds * kBlock];
+  extern __shared__ int s_stack[];  // sc.stack entries per lane (stack_lds_bytes)
   const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
   if (i >= n) return;
   const f3 o = f3{rays[i], rays[(size_t)n + i], rays[2 * (size_t)n + i]};
@@ -210,34 +266,109 @@ k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __res
   dist[i] = h.dist;
 }
 
+// LPT order of the pixel blocks from the pre-pass costs, one workgroup: bucket
+// by floor(log2(cost)), most expensive bucket first (order within a bucket is
+// arbitrary: the order only shapes the schedule, never a pixel's result).
+constexpr int kLptThreads = 1024, kLptBuckets = 33;
+__global__ void __launch_bounds__(kLptThreads)
+k_lpt_order(const uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __restrict__ perm) {
+  __shared__ uint32_t s_cnt[kLptBuckets], s_off[kLptBuckets];
+  if (threadIdx.x < kLptBuckets) s_cnt[threadIdx.x] = 0;
+  __syncthreads();
+  auto bucket = [](uint32_t c) { return c ? 32u - (uint32_t)__clz((int)c) : 0u; };  // 0..32, higher = costlier
+  for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) atomicAdd(&s_cnt[bucket(cost[i])], 1u);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t run = 0;
+    for (int b = kLptBuckets - 1; b >= 0; --b) {
+      s_off[b] = run;
+      run += s_cnt[b];
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) perm[atomicAdd(&s_off[bucket(cost[i])], 1u)] = i;
+}
+
 hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
                          uchar4* out8, float4* out32, uint32_t* outhit,
-                         unsigned long long* counters, hipStream_t stream) {
+                         unsigned long long* counters, uint32_t resident, hipStream_t stream) {
   const uint32_t bx = (fr.tw + 7u) / 8u, by = (fr.th + 7u) / 8u;
   const uint64_t blocks = (uint64_t)bx * by * fr.n_tiles;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
-  const dim3 grid((uint32_t)blocks), block(kBlock);
+  const dim3 block(kBlock);
+  const size_t lds = stack_lds_bytes(sc);
   const bool tris = sc.n_tris > 0;
-  const bool ps = tris && fr.kernel == 2;
+  if (tris && fr.kernel == 2) {
+    if (blocks * 64ull > 0xffffffffull || resident == 0) return hipErrorInvalidValue;
+    const uint32_t nb = (uint32_t)blocks;
+    const dim3 grid(nb < resident ? nb : resident);
+    // per-launch workspace (stream-ordered, so concurrent launches never share
+    // it): [0] pre-pass queue, [1] queue, then cost[nb], perm[nb]
+    const bool lpt = fr.pq_lpt && fr.sqrt_spp >= 2;
+    const size_t ws_bytes = 256 + (lpt ? 8ull * nb : 0);
+    void* ws = nullptr;
+    hipError_t e = hipMallocAsync(&ws, ws_bytes, stream);
+    if (e != hipSuccess) return e;
+    uint32_t* q = (uint32_t*)ws;
+    DevFrame f = fr;
+    f.n_slots = nb * 64u;
+    f.perm = nullptr;
+    f.cost = nullptr;
+    e = hipMemsetAsync(ws, 0, 256 + (lpt ? 4ull * nb : 0), stream);
+    if (e == hipSuccess && lpt) {
+      DevFrame fc = f;
+      fc.sqrt_spp = 1;
+      fc.recip_sqrt_spp = 1.0f;
+      fc.fspp = 1.0f;
+      fc.cost = (uint32_t*)((char*)ws + 256);
+      k_render_ps<false, true><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
+      k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb);
+      f.perm = fc.cost + nb;
+      e = hipGetLastError();
+    }
+    if (e == hipSuccess) {
+      if (counters) k_render_ps<true, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, counters, q + 1);
+      else k_render_ps<false, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
+      e = hipGetLastError();
+    }
+    const hipError_t ef = hipFreeAsync(ws, stream);
+    return e != hipSuccess ? e : ef;
+  }
+  const dim3 grid((uint32_t)blocks);
   if (counters) {
-    if (ps) k_render_ps<true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
-    else if (tris) k_render<true, true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
-    else k_render<false, true><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
+    if (tris) k_render<true, true><<<grid, block, lds, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
+    else k_render<false, true><<<grid, block, lds, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
   } else {
-    if (ps) k_render_ps<false><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
-    else if (tris) k_render<true, false><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
-    else k_render<false, false><<<grid, block, 0, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
+    if (tris) k_render<true, false><<<grid, block, lds, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
+    else k_render<false, false><<<grid, block, lds, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
   }
   return hipGetLastError();
+}
+
+hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
+  int per_cu_plain = 0, per_cu_stats = 0, cus = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu_plain, reinterpret_cast<const void*>(&k_render_ps<false, false>), kBlock, stack_lds_bytes(sc));
+  if (e != hipSuccess) return e;
+  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu_stats, reinterpret_cast<const void*>(&k_render_ps<true, false>), kBlock, stack_lds_bytes(sc));
+  if (e != hipSuccess) return e;
+  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess) return e;
+  // the larger of the two variants' capacities: waves beyond a variant's capacity
+  // start as others retire and find the queue drained or nearly so
+  const int per_cu = per_cu_plain > per_cu_stats ? per_cu_plain : per_cu_stats;
+  waves = (uint32_t)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1));
+  return hipSuccess;
 }
 
 hipError_t launch_trace(const DevScene& sc, const float* d_rays, uint32_t n, uint32_t* prim,
                         float* dist, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const dim3 grid((n + kBlock - 1) / kBlock), block(kBlock);
-  if (sc.n_tris > 0) k_trace<true><<<grid, block, 0, stream>>>(sc, d_rays, n, prim, dist);
-  else k_trace<false><<<grid, block, 0, stream>>>(sc, d_rays, n, prim, dist);
+  if (sc.n_tris > 0) k_trace<true><<<grid, block, stack_lds_bytes(sc), stream>>>(sc, d_rays, n, prim, dist);
+  else k_trace<false><<<grid, block, stack_lds_bytes(sc), stream>>>(sc, d_rays, n, prim, dist);
   return hipGetLastError();
 }
 

@@ -48,6 +48,7 @@ struct wgt_ctx {
   // wavefront path state + completion counter (device) and its pinned mirror
   DevBuf wf, ctl;
   unsigned long long* ctl_host = nullptr;
+  uint32_t ps_resident = 0;  // resident k_render_ps waves for the current scene
   std::vector<hipEvent_t> evpool;  // per-launch timing (profile runs only)
 };
 
@@ -130,6 +131,9 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
   fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
+  fr.pq_refill = env_u32("WGT_PQ_REFILL", 8);
+  fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);  // 0: row order (A/B), else LPT order from a 1-spp pre-pass
+  if (fr.pq_refill < 1) fr.pq_refill = 1;
   return fr;
 }
 
@@ -187,7 +191,7 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
     hipEvent_t e0 = timing ? pool_event(ctx, 0) : nullptr, e1 = timing ? pool_event(ctx, 1) : nullptr;
     if (timing && (!e0 || !e1)) return fail(ctx, WGT_E_HIP, "hipEventCreate failed");
     if (timing) WGT_HIP(ctx, hipEventRecord(e0, s));
-    WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, s));
+    WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident, s));
     if (timing) {
       WGT_HIP(ctx, hipEventRecord(e1, s));
       WGT_HIP(ctx, hipEventSynchronize(e1));
@@ -321,6 +325,34 @@ int wgt_sync(wgt_ctx* ctx) {
   return WGT_OK;
 }
 
+// Host-only: build the BVH exactly as wgt_upload_scene does and export it.
+int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, uint32_t nodes_cap,
+                  float* tris_out, wgt_scene_info* info) {
+  if (!tris || n_tris == 0 || !info) return fail(nullptr, WGT_E_INVALID, "null triangles or info");
+  BvhOut bvh;
+  std::string err;
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, (uint32_t)kStackMax, bvh, err))
+    return fail(nullptr, WGT_E_INVALID, err);
+  *info = wgt_scene_info{};
+  info->n_tris = n_tris;
+  info->bvh_nodes = bvh.n_nodes;
+  info->bvh_leaves = bvh.n_leaves;
+  info->bvh_max_depth = bvh.max_depth;
+  info->bvh_max_leaf = bvh.max_leaf;
+  info->device_bytes = (bvh.nodes.size() + bvh.tris.size() + bvh.tshade.size()) * 4;
+  info->sah_cost = bvh.sah_cost;
+  info->bvh_width = (uint32_t)kBvhWidth;
+  info->bvh_stack = bvh.stack_need > 0 ? bvh.stack_need : 1u;
+  info->bvh2_nodes = bvh.n_nodes2;
+  info->bvh2_depth = bvh.depth2;
+  if (nodes_out) {
+    if (nodes_cap < bvh.n_nodes) return fail(nullptr, WGT_E_INVALID, "node capacity too small");
+    std::memcpy(nodes_out, bvh.nodes.data(), bvh.nodes.size() * 4);
+  }
+  if (tris_out) std::memcpy(tris_out, bvh.tris.data(), bvh.tris.size() * 4);
+  return WGT_OK;
+}
+
 int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, const wgt_quad* quads,
                      uint32_t n_quads, const wgt_sphere* spheres, uint32_t n_spheres,
                      const wgt_triangle* tris, uint32_t n_tris) {
@@ -336,7 +368,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   BvhOut bvh;
   if (n_tris > 0) {
     std::string err;
-    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, bvh, err)) return fail(ctx, WGT_E_INVALID, err);
+    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, (uint32_t)kStackMax, bvh, err)) return fail(ctx, WGT_E_INVALID, err);
   }
   const uint32_t nlq = n_lights + n_quads;
   const size_t b_quads = align256((size_t)nlq * 96);
@@ -382,7 +414,9 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const f3 lr = f3{lights[0].right[0], lights[0].right[1], lights[0].right[2]};
   const f3 lu = f3{lights[0].up[0], lights[0].up[1], lights[0].up[2]};
   sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
-  sc.max_iters = 2u * bvh.n_nodes + 8u;
+  sc.max_iters = 4u * bvh.n_nodes + 8u;
+  sc.stack = bvh.stack_need > 0 ? bvh.stack_need : 1u;
+  WGT_HIP(ctx, ps_resident_waves(sc, ctx->device, ctx->ps_resident));
 
   wgt_scene_info& in = ctx->info;
   in = wgt_scene_info{};
@@ -396,6 +430,10 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   in.bvh_max_leaf = bvh.max_leaf;
   in.device_bytes = total;
   in.sah_cost = bvh.sah_cost;
+  in.bvh_width = n_tris ? (uint32_t)kBvhWidth : 0u;
+  in.bvh_stack = n_tris ? sc.stack : 0u;
+  in.bvh2_nodes = bvh.n_nodes2;
+  in.bvh2_depth = bvh.depth2;
   ctx->has_scene = true;
   return WGT_OK;
 }

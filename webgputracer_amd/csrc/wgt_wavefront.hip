@@ -29,7 +29,6 @@ namespace wgt {
 enum : uint32_t { PH_NEED = 0u, PH_WAIT = 1u, PH_DONE = 2u };
 
 constexpr int kWfShadeBlock = 256;
-constexpr int kWfStack = kStackLds;  // LDS stack entries per lane in k_wf_trace
 constexpr int kWfChunkMax = 1024;
 
 
@@ -84,16 +83,15 @@ k_wf_init(DevFrame fr, const wgt_tile* __restrict__ tiles, WfState st, uchar4* _
 
 // The first traversal step on the root decides whether a ray needs the BVH at all.
 __device__ __forceinline__ bool root_needs_trav(const DevScene& sc, f3 o, f3 d, bool quad_hit, float qt) {
-  const f3 inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
-  const f3 ot = slab_offset(o, inv);
-  const float bt = quad_hit ? qt : kRayMax;
-  const float4 a = sc.nodes[0], b = sc.nodes[1], c = sc.nodes[2];
-  float n0, f0, n1, f1;
-  slab(ot, inv, f3{a.x, a.z, c.x}, f3{a.y, a.w, c.y}, n0, f0);
-  slab(ot, inv, f3{b.x, b.z, c.z}, f3{b.y, b.w, c.w}, n1, f1);
-  const bool h0 = (n0 <= f0) & (n0 <= bt) & (f0 >= kRayMin);
-  const bool h1 = (n1 <= f1) & (n1 <= bt) & (f1 >= kRayMin);
-  return h0 || h1;
+  Trav t;
+  trav_init(o, d, quad_hit, qt, t);
+  const float4* __restrict__ n = sc.nodes;
+  const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
+  const uint32_t k0 = child_key(t, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, 0u);
+  const uint32_t k1 = child_key(t, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, 1u);
+  const uint32_t k2 = child_key(t, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, 2u);
+  const uint32_t k3 = child_key(t, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, 3u);
+  return (k0 & k1 & k2 & k3) != kMissKey;  // a hit key has bit 31 clear
 }
 
 template <bool STATS>
@@ -122,7 +120,7 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
   f3 pc = ld3(st.pc, n, s);
   f3 ro = ld3(st.ro, n, s);
   f3 rd = ld3(st.rd, n, s);
-  Counters c{0u, 0u, 0u, 0u, 0u};
+  Counters c{0u, 0u, 0u, 0u, 0u, 0u};
   TravStats ts{0u, 0u, 0u, 0u};
 
   auto shade_and_advance = [&](const Hit& h) {
@@ -222,7 +220,7 @@ template <bool STATS>
 __global__ void __launch_bounds__(kBlock)
 k_wf_trace(DevScene sc, DevFrame fr, WfState st, unsigned long long* __restrict__ counters) {
   __shared__ uint32_t s_list[kWfChunkMax];
-  __shared__ int s_stack[kWfStack * kBlock];
+  extern __shared__ int s_stack[];  // sc.stack entries per lane (stack_lds_bytes)
   const uint32_t C = fr.wf_chunk;
   const uint32_t base = blockIdx.x * C;
   if (base >= st.n) return;
@@ -264,7 +262,7 @@ k_wf_trace(DevScene sc, DevFrame fr, WfState st, unsigned long long* __restrict_
       next += n_idle;
     }
     if (!__any(active)) break;
-    if (active && trav_step<STATS, kWfStack>(sc, o, d, t, lds, ts)) {
+    if (active && trav_step<STATS>(sc, o, d, t, lds, ts)) {
       st.res_i[slot] = t.found ? t.bi : kNoHit;
       st.res_t[slot] = t.bt;
       active = false;
@@ -324,8 +322,8 @@ hipError_t launch_wf_trace(const DevScene& sc, const DevFrame& fr, const WfState
   if (fr.wf_chunk == 0 || fr.wf_chunk > (uint32_t)kWfChunkMax || fr.wf_chunk % kBlock != 0)
     return hipErrorInvalidValue;
   const dim3 grid((st.n + fr.wf_chunk - 1) / fr.wf_chunk), block(kBlock);
-  if (counters) k_wf_trace<true><<<grid, block, 0, stream>>>(sc, fr, st, counters);
-  else k_wf_trace<false><<<grid, block, 0, stream>>>(sc, fr, st, nullptr);
+  if (counters) k_wf_trace<true><<<grid, block, stack_lds_bytes(sc), stream>>>(sc, fr, st, counters);
+  else k_wf_trace<false><<<grid, block, stack_lds_bytes(sc), stream>>>(sc, fr, st, nullptr);
   return hipGetLastError();
 }
 

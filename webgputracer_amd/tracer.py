@@ -84,6 +84,18 @@ def mesh_scene(kind: str, target_tris: int | None = None, seed: int = 1, obj_pat
     return lights, quads[:5].copy(), spheres, tris
 
 
+def bvh_build(tris):
+    """Host-only BVH build (wgt_bvh_build): (info, nodes (n, 8, 4) f32, leaf-ordered tris (n, 4, 4) f32)."""
+    tris = np.ascontiguousarray(tris, TRI_DTYPE)
+    L = lib()
+    info = WgtSceneInfo()
+    check(L.wgt_bvh_build(ptr(tris), len(tris), None, 0, None, ctypes.byref(info)))
+    nodes = np.zeros((info.bvh_nodes, 8, 4), np.float32)
+    recs = np.zeros((len(tris), 4, 4), np.float32)
+    check(L.wgt_bvh_build(ptr(tris), len(tris), ptr(nodes), info.bvh_nodes, ptr(recs), ctypes.byref(info)))
+    return info.as_dict(), nodes, recs
+
+
 def camera_param(aspect: float, spp: int, seed: int, fovy: float = 40.0):
     """Camera::Update (camera.cpp:64-70) with an explicit seed instead of RandSeed()."""
     cam = np.zeros(1, CAMERA_DTYPE)
