@@ -10,8 +10,10 @@ rank 0 (RCCL over xGMI) and assembled — weak scaling, per-GPU work fixed.
 value = closest-hit queries actually traced (non-NaN rays, counted on the device by
 an instrumented pass over the same tiles) summed over ranks x steps / max-over-ranks
 wall time of the K timed steps.  Scene/BVH upload and tile lists are resident in HBM
-before timing.  The kernel is launched on torch's current stream so torch.cuda.Event
-pairs time exactly the render launches (roofline.achieved).
+before timing.  The render call is launched on torch's current stream so
+torch.cuda.Event pairs time exactly its launches (roofline.achieved): the 1-spp cost
+pre-pass + LPT ordering (~0.5 % of the call at 256 spp) and the main kernel
+k_render_ps (the rocprof kernel trace under profiles/ lists them separately).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scene bunny|sponza|cornell]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -31,7 +33,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/sec at 1080p/256spp + achieved HBM GB/s vs peak, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
-NODE_BYTES, TRI_BYTES, SHADE_BYTES = 64, 48, 32  # algorithmic bytes per unit
+# algorithmic bytes per unit: a BVH4 node visit reads 7 x 16 B (6 SoA
+# box rows + child refs) of its 128-B line, a triangle test 3 x 16 B of its 64-B
+# record (the 4th, the padded box, only for a candidate closest hit), a traced ray
+# 32 B of per-triangle shading data
+NODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 48, 32
+DOMINANT_KERNEL = "wgt::k_render_ps<false, false>"
 
 
 def parse():
@@ -185,14 +192,15 @@ def main():
 
     base = cpu_baseline(args, scene, rank, world)
     if rank == 0:
-        # dominant kernel = k_render<true,false>; algorithmic bytes of rank 0's launch
+        # dominant kernel = DOMINANT_KERNEL; algorithmic bytes of rank 0's launch
         bytes_launch = (mine[4] * NODE_BYTES + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if tj.get("workload") == f"{args.scene}-{W}x{H}-{spp}spp" and tj.get("n_gpus", 1) == 1 and world == 1:
+            if (tj.get("workload") == f"{args.scene}-{W}x{H}-{spp}spp" and tj.get("n_gpus", 1) == 1 and world == 1
+                    and tj.get("kernel") == DOMINANT_KERNEL):
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass

@@ -62,7 +62,9 @@ def main():
             v /= max(calls[k], 1)
             per[(k, c)] = v
             out.append(f"| `{k}` | {c} | {v:,.1f} |")
-    timed = "wgt::k_render<true, false>"
+    sys.path.insert(0, ROOT)
+    from bench import DOMINANT_KERNEL
+    timed = DOMINANT_KERNEL
     fetch = per.get((timed, "FETCH_SIZE"))
     write = per.get((timed, "WRITE_SIZE"))
     if fetch is not None and write is not None:
