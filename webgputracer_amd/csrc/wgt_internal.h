@@ -64,12 +64,14 @@ struct DevFrame {
   // idle lanes that trigger a refill from the wave's ray list
   uint32_t wf_rays, wf_chunk, wf_refill;
   // persistent k_render_ps: pixel slots of the launch (64 per 8x8 block), the
-  // idle lanes that trigger a refill from the pixel queue, LPT ordering on/off,
+  // idle lanes that trigger a refill from the pixel queue, LPT ordering (0 = off,
+  // n = order from an n*n-spp cost pre-pass),
   // the queue order (queue block q renders pixel block perm[q]; NULL = identity)
   // and the pre-pass cost per pixel block (set by launch_render)
   uint32_t n_slots, pq_refill, pq_lpt;
   const uint32_t* perm;
   uint32_t* cost;
+
 };
 
 // Wavefront path state, SoA over slots (one slot per pixel of the tile list).
@@ -119,9 +121,13 @@ enum {
 // k_render_ps runs persistent: at most `resident` waves (ps_resident_waves),
 // lanes pulling pixel slots from a per-launch queue in LPT order (1-spp cost
 // pre-pass + k_lpt_order), all stream-ordered on `stream`.
+// ws: scheduling workspace of >= render_ws_bytes(fr) bytes, used in stream order
+// (one launch in flight per workspace).
+size_t render_ws_bytes(const DevFrame& fr);
 hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
                          uchar4* out8, float4* out32, uint32_t* outhit,
-                         unsigned long long* counters, uint32_t resident, hipStream_t stream);
+                         unsigned long long* counters, uint32_t resident, void* ws, size_t ws_cap,
+                         hipStream_t stream);
 // Waves of k_render_ps resident on the whole device for this scene's LDS stack.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves);
 hipError_t launch_trace(const DevScene& sc, const float* d_rays, uint32_t n, uint32_t* prim,

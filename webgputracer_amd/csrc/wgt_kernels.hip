@@ -267,31 +267,39 @@ k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __res
 }
 
 // LPT order of the pixel blocks from the pre-pass costs, one workgroup: bucket
-// by floor(log2(cost)), most expensive bucket first (order within a bucket is
-// arbitrary: the order only shapes the schedule, never a pixel's result).
-constexpr int kLptThreads = 1024, kLptBuckets = 33;
+// by the float bits of the cost (exponent + 3 mantissa bits: 8 buckets per
+// octave), most expensive bucket first (order within a bucket is arbitrary: the
+// order only shapes the schedule, never a pixel's result).
+constexpr int kLptThreads = 1024, kLptBuckets = 1280;  // float bits >> 20 of any u32 cost
+__device__ __forceinline__ uint32_t lpt_bucket(uint32_t c) { return __float_as_uint((float)c) >> 20; }
 __global__ void __launch_bounds__(kLptThreads)
 k_lpt_order(const uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __restrict__ perm) {
-  __shared__ uint32_t s_cnt[kLptBuckets], s_off[kLptBuckets];
-  if (threadIdx.x < kLptBuckets) s_cnt[threadIdx.x] = 0;
+  __shared__ uint32_t s_cnt[kLptBuckets];
+  for (int b = threadIdx.x; b < kLptBuckets; b += kLptThreads) s_cnt[b] = 0;
   __syncthreads();
-  auto bucket = [](uint32_t c) { return c ? 32u - (uint32_t)__clz((int)c) : 0u; };  // 0..32, higher = costlier
-  for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) atomicAdd(&s_cnt[bucket(cost[i])], 1u);
+  for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) atomicAdd(&s_cnt[lpt_bucket(cost[i])], 1u);
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // exclusive scan from the most expensive bucket down
     uint32_t run = 0;
     for (int b = kLptBuckets - 1; b >= 0; --b) {
-      s_off[b] = run;
-      run += s_cnt[b];
+      const uint32_t n = s_cnt[b];
+      s_cnt[b] = run;
+      run += n;
     }
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) perm[atomicAdd(&s_off[bucket(cost[i])], 1u)] = i;
+  for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) perm[atomicAdd(&s_cnt[lpt_bucket(cost[i])], 1u)] = i;
+}
+
+size_t render_ws_bytes(const DevFrame& fr) {
+  const uint64_t bx = (fr.tw + 7u) / 8u, by = (fr.th + 7u) / 8u;
+  return 256 + 8 * bx * by * fr.n_tiles;
 }
 
 hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
                          uchar4* out8, float4* out32, uint32_t* outhit,
-                         unsigned long long* counters, uint32_t resident, hipStream_t stream) {
+                         unsigned long long* counters, uint32_t resident, void* ws, size_t ws_cap,
+                         hipStream_t stream) {
   const uint32_t bx = (fr.tw + 7u) / 8u, by = (fr.th + 7u) / 8u;
   const uint64_t blocks = (uint64_t)bx * by * fr.n_tiles;
   if (blocks == 0) return hipSuccess;
@@ -301,26 +309,23 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   const bool tris = sc.n_tris > 0;
   if (tris && fr.kernel == 2) {
     if (blocks * 64ull > 0xffffffffull || resident == 0) return hipErrorInvalidValue;
+    if (!ws || ws_cap < render_ws_bytes(fr)) return hipErrorInvalidValue;
     const uint32_t nb = (uint32_t)blocks;
     const dim3 grid(nb < resident ? nb : resident);
-    // per-launch workspace (stream-ordered, so concurrent launches never share
-    // it): [0] pre-pass queue, [1] queue, then cost[nb], perm[nb]
-    const bool lpt = fr.pq_lpt && fr.sqrt_spp >= 2;
-    const size_t ws_bytes = 256 + (lpt ? 8ull * nb : 0);
-    void* ws = nullptr;
-    hipError_t e = hipMallocAsync(&ws, ws_bytes, stream);
-    if (e != hipSuccess) return e;
+    // workspace (the context's, used in stream order): [0] pre-pass queue,
+    // [1] queue | cost[nb] | perm[nb]
+    const bool lpt = fr.pq_lpt && fr.sqrt_spp > fr.pq_lpt;
     uint32_t* q = (uint32_t*)ws;
     DevFrame f = fr;
     f.n_slots = nb * 64u;
     f.perm = nullptr;
     f.cost = nullptr;
-    e = hipMemsetAsync(ws, 0, 256 + (lpt ? 4ull * nb : 0), stream);
+    hipError_t e = hipMemsetAsync(ws, 0, 256 + (lpt ? 4ull * nb : 0), stream);
     if (e == hipSuccess && lpt) {
-      DevFrame fc = f;
-      fc.sqrt_spp = 1;
-      fc.recip_sqrt_spp = 1.0f;
-      fc.fspp = 1.0f;
+      DevFrame fc = f;  // the pre-pass: fr.pq_lpt^2 samples per pixel
+      fc.sqrt_spp = fr.pq_lpt < fr.sqrt_spp ? fr.pq_lpt : fr.sqrt_spp;
+      fc.recip_sqrt_spp = 1.0f / (float)fc.sqrt_spp;
+      fc.fspp = (float)(fc.sqrt_spp * fc.sqrt_spp);
       fc.cost = (uint32_t*)((char*)ws + 256);
       k_render_ps<false, true><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
       k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb);
@@ -332,8 +337,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       else k_render_ps<false, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
       e = hipGetLastError();
     }
-    const hipError_t ef = hipFreeAsync(ws, stream);
-    return e != hipSuccess ? e : ef;
+    return e;
   }
   const dim3 grid((uint32_t)blocks);
   if (counters) {

@@ -48,7 +48,9 @@ struct wgt_ctx {
   // wavefront path state + completion counter (device) and its pinned mirror
   DevBuf wf, ctl;
   unsigned long long* ctl_host = nullptr;
-  uint32_t ps_resident = 0;  // resident k_render_ps waves for the current scene
+  uint32_t ps_resident = 0;
+  DevBuf ws;  // scheduling workspace of the persistent kernel (queues, LPT costs and order)
+  hipEvent_t ws_ev = nullptr;  // recorded after each launch that used ws  // resident k_render_ps waves for the current scene
   std::vector<hipEvent_t> evpool;  // per-launch timing (profile runs only)
 };
 
@@ -132,7 +134,8 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
   fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
   fr.pq_refill = env_u32("WGT_PQ_REFILL", 8);
-  fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);  // 0: row order (A/B), else LPT order from a 1-spp pre-pass
+  // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
+  fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   if (fr.pq_refill < 1) fr.pq_refill = 1;
   return fr;
 }
@@ -191,7 +194,17 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
     hipEvent_t e0 = timing ? pool_event(ctx, 0) : nullptr, e1 = timing ? pool_event(ctx, 1) : nullptr;
     if (timing && (!e0 || !e1)) return fail(ctx, WGT_E_HIP, "hipEventCreate failed");
     if (timing) WGT_HIP(ctx, hipEventRecord(e0, s));
-    WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident, s));
+    int rc;
+    const size_t ws_need = render_ws_bytes(fr);
+    if (ctx->ws.bytes < ws_need && ctx->ws_ev) WGT_HIP(ctx, hipEventSynchronize(ctx->ws_ev));  // before regrowing
+    if ((rc = ensure(ctx, ctx->ws, ws_need))) return rc;
+    // the workspace is the context's: a launch on any stream first waits for the
+    // previous launch that used it (calls on one context serialise on the device)
+    if (!ctx->ws_ev) WGT_HIP(ctx, hipEventCreateWithFlags(&ctx->ws_ev, hipEventDisableTiming));
+    else WGT_HIP(ctx, hipStreamWaitEvent(s, ctx->ws_ev, 0));
+    WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
+                               ctx->ws.p, ctx->ws.bytes, s));
+    WGT_HIP(ctx, hipEventRecord(ctx->ws_ev, s));
     if (timing) {
       WGT_HIP(ctx, hipEventRecord(e1, s));
       WGT_HIP(ctx, hipEventSynchronize(e1));
@@ -307,7 +320,8 @@ void wgt_destroy(wgt_ctx* ctx) {
   if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
   free_buf(ctx->tiles); free_buf(ctx->out8); free_buf(ctx->out32); free_buf(ctx->hit);
   free_buf(ctx->counters); free_buf(ctx->rays); free_buf(ctx->prim); free_buf(ctx->dist);
-  free_buf(ctx->wf); free_buf(ctx->ctl);
+  free_buf(ctx->wf); free_buf(ctx->ctl); free_buf(ctx->ws);
+  if (ctx->ws_ev) (void)hipEventDestroy(ctx->ws_ev);
   if (ctx->ctl_host) (void)hipHostFree(ctx->ctl_host);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
