@@ -117,6 +117,10 @@ typedef struct {
   float trace_ms;        /* ... of which BVH-traversal kernel launches (wavefront) */
   float shade_ms;        /* ... of which shading kernel launches (wavefront) */
   uint32_t iterations;   /* wavefront bounce iterations (1 for a megakernel launch) */
+  /* phase-split kernel: wave cycles of the service phase by region: pixel refill +
+   * writes, finalise (quad rebuild, triangle merge, spheres), shading, camera ray +
+   * NaN handling, quad scan, root-node test */
+  uint64_t cyc_refill, cyc_finalise, cyc_shade, cyc_camera, cyc_quads, cyc_root;
 } wgt_stats;
 
 typedef struct {

@@ -1,5 +1,5 @@
-"""Sweep the phase-split thresholds / kernel choice on one GPU (one process).
-  python scripts/sweep_ps.py [scene] [W H spp]"""
+"""Sweep the phase-split thresholds of the persistent kernel (one process, one GPU).
+  python scripts/sweep_ps.py [scene W H spp]"""
 import itertools
 import json
 import os
@@ -14,21 +14,11 @@ W, H, spp = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 108
 ctx = w.Context(0)
 ctx.upload_scene(*w.mesh_scene(scene))
 cam = w.camera_param(W / H, spp, 0)
-ref = None
-configs = [("1", None, None)] + [("0", str(x), str(y)) for x, y in itertools.product([24, 32, 40, 48, 56], [8, 16, 24])
-                                   if y < x]
-for kern, x, y in configs:
-    os.environ["WGT_KERNEL"] = kern
-    if x:
-        os.environ["WGT_PS_TO_TRAV"], os.environ["WGT_PS_TO_SERVICE"] = x, y
-    ctx.render_tile(cam, W, H, want=("u8",))  # warm
-    r = ctx.render_tile(cam, W, H, want=("u8",), stats=True)
-    st = r["stats"]
-    same = ref is None or (r["u8"] == ref).all()
-    ref = r["u8"] if ref is None else ref
-    print(json.dumps({"kernel": kern, "to_trav": x, "to_service": y, "ms": round(st["kernel_ms"], 2),
-                      "Mrays_s": round(st["traced_rays"] / st["kernel_ms"] / 1e3, 1),
-                      "svc_util": round(st["loop_lane_iters"] / max(64 * st["loop_wave_iters"], 1), 3),
-                      "trav_util": round(st["trav_lane_steps"] / max(64 * st["trav_wave_steps"], 1), 3),
-                      "identical": bool(same)}), flush=True)
+grid = [(t, s) for t, s in itertools.product(
+    [int(v) for v in os.environ.get("PS_T", "16,24,32,40,48").split(",")],
+    [int(v) for v in os.environ.get("PS_S", "4,8,12,16").split(",")]) if s < t]
+for t, s in [(24, 8)] + grid:
+    os.environ["WGT_PS_TO_TRAV"], os.environ["WGT_PS_TO_SERVICE"] = str(t), str(s)
+    ms = min(ctx.render_tile(cam, W, H, want=("u8",), stats=True)["stats"]["kernel_ms"] for _ in range(2))
+    print(json.dumps({"scene": scene, "to_trav": t, "to_service": s, "ms": round(ms, 2)}), flush=True)
 ctx.close()

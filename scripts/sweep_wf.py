@@ -47,5 +47,8 @@ for cfg in configs:
                       "trav_cyc_per_step": round(st["cyc_trav"] / max(st["trav_wave_steps"], 1), 1),
                       "wave_iters": st["loop_wave_iters"], "wave_steps": st["trav_wave_steps"],
                       "nodes": st["node_visits"], "tris": st["tri_tests"], "rays": st["traced_rays"],
+                      "svc_regions": {k[4:]: round(st[k] / max(st["cyc_service"], 1), 3) for k in
+                                      ("cyc_refill", "cyc_finalise", "cyc_shade", "cyc_camera", "cyc_quads",
+                                       "cyc_root")},
                       "identical": bool(same)}), flush=True)
 ctx.close()

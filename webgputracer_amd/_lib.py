@@ -37,7 +37,10 @@ class WgtStats(ctypes.Structure):
                 ("loop_lane_iters", ctypes.c_uint64), ("trav_wave_steps", ctypes.c_uint64),
                 ("trav_lane_steps", ctypes.c_uint64), ("cyc_service", ctypes.c_uint64),
                 ("cyc_trav", ctypes.c_uint64), ("kernel_ms", ctypes.c_float),
-                ("trace_ms", ctypes.c_float), ("shade_ms", ctypes.c_float), ("iterations", ctypes.c_uint32)]
+                ("trace_ms", ctypes.c_float), ("shade_ms", ctypes.c_float), ("iterations", ctypes.c_uint32),
+                ("cyc_refill", ctypes.c_uint64), ("cyc_finalise", ctypes.c_uint64),
+                ("cyc_shade", ctypes.c_uint64), ("cyc_camera", ctypes.c_uint64), ("cyc_quads", ctypes.c_uint64),
+                ("cyc_root", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

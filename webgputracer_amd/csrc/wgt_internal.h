@@ -114,7 +114,13 @@ enum {
   CNT_TRAV_LANE,
   CNT_CYC_SERVICE,  // s_memtime cycles per wave spent in each phase (instrumented pass)
   CNT_CYC_TRAV,
-  CNT_N = 14
+  CNT_CYC_REFILL,  // service-phase regions (k_render_ps, instrumented pass)
+  CNT_CYC_FINALISE,
+  CNT_CYC_SHADE,
+  CNT_CYC_CAMERA,
+  CNT_CYC_QUADS,
+  CNT_CYC_ROOT,
+  CNT_N = 20
 };
 
 // Launchers implemented in wgt_kernels.hip

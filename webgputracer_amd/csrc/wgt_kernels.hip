@@ -92,6 +92,15 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
 // COST: the 1-spp pre-pass: no output, each finished pixel adds its work units
 // (kCostService per ray started + 1 per traversal step) to fr.cost[its block].
 constexpr uint32_t kCostService = 7;  // a service iteration ~ 7 traversal steps (profiles/)
+// STATS: wave cycles per service-phase region (s_memtime; the regions run in
+// divergent code, so each adds the wave's time spent issuing or waiting in it).
+#define WGT_REGION(acc, ...)                                  \
+  do {                                                        \
+    const uint64_t r0_ = STATS ? __builtin_amdgcn_s_memtime() : 0; \
+    __VA_ARGS__;                                              \
+    if (STATS) acc += __builtin_amdgcn_s_memtime() - r0_;     \
+  } while (0)
+
 template <bool STATS, bool COST>
 __global__ void __launch_bounds__(kBlock)
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
@@ -117,12 +126,14 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   bool exhausted = false;  // the queue is empty for this lane
   bool trav = false, pending = false, fin = false;
   uint64_t cyc_svc = 0, cyc_trav = 0;
+  uint64_t cr_refill = 0, cr_fin = 0, cr_shade = 0, cr_cam = 0, cr_quads = 0, cr_root = 0;
   uint32_t pblock = 0, work = 0;  // COST: the pixel's block and its work so far
 
   for (;;) {
     // ------------------------------------------------------------ service phase
     uint64_t t_phase = STATS ? __builtin_amdgcn_s_memtime() : 0;
     for (;;) {
+      const uint64_t tr0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
       if (fin) {  // a finished pixel: write it (here, outside the sample loop)
         if (COST) {
           atomicAdd(fr.cost + pblock, work);
@@ -157,6 +168,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           }
         }
       }
+      if (STATS) cr_refill += __builtin_amdgcn_s_memtime() - tr0;
       const bool need = have && !trav;
       if (!__any(need)) {
         if (__ballot(!have && !exhausted) != 0ull && __ballot(trav) == 0ull) continue;  // refill again
@@ -167,16 +179,17 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
         if (pending) {
           // finalise: rebuild the quad hit, merge triangles, scan spheres, shade
           Hit h;
-          quad_rebuild(sc, ro, rd, q_prim, q_t, h);
-          finish_hit(sc, ro, rd, t, h);
+          WGT_REGION(cr_fin, quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h));
           if (STATS) { ++c.q; ++c.tr; }
           if (px.k == 0 && depth == 0) px.hit0 = h.prim;
+          const uint64_t ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
           const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
           ++depth;
           if (end || depth == kRayDepth) {
             end_sample(fr, px, pc);
             depth = 0;
           }
+          if (STATS) cr_shade += __builtin_amdgcn_s_memtime() - ts0;
           pending = false;
         }
         // start the next ray of this pixel
@@ -187,7 +200,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             break;
           }
           if (depth == 0) {
-            camera_ray(fr, px, ro, rd);
+            WGT_REGION(cr_cam, camera_ray(fr, px, ro, rd));
             pc = f3{1.0f, 1.0f, 1.0f};
           }
           if (has_nan(ro) || has_nan(rd)) {
@@ -209,13 +222,14 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             continue;
           }
           Hit h;
-          quad_scan(sc, ro, rd, h, q_t);
-          q_prim = h.prim;
-          trav_init(ro, rd, q_prim != kNoHit, q_t, t);
+          WGT_REGION(cr_quads, quad_scan(sc, ro, rd, h, q_t); q_prim = h.prim;
+                     trav_init(ro, rd, q_prim != kNoHit, q_t, t));
           if (COST) work += kCostService;
           // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
-          if (trav_step<STATS>(sc, ro, rd, t, lds, st)) pending = true;
+          bool done_root = false;
+          WGT_REGION(cr_root, done_root = trav_step<STATS>(sc, ro, rd, t, lds, st));
+          if (done_root) pending = true;
           else trav = true;
           break;
         }
@@ -246,6 +260,12 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
     if (lane == 0) {
       atomicAdd(&counters[CNT_CYC_SERVICE], (unsigned long long)cyc_svc);
       atomicAdd(&counters[CNT_CYC_TRAV], (unsigned long long)cyc_trav);
+      atomicAdd(&counters[CNT_CYC_REFILL], (unsigned long long)cr_refill);
+      atomicAdd(&counters[CNT_CYC_FINALISE], (unsigned long long)cr_fin);
+      atomicAdd(&counters[CNT_CYC_SHADE], (unsigned long long)cr_shade);
+      atomicAdd(&counters[CNT_CYC_CAMERA], (unsigned long long)cr_cam);
+      atomicAdd(&counters[CNT_CYC_QUADS], (unsigned long long)cr_quads);
+      atomicAdd(&counters[CNT_CYC_ROOT], (unsigned long long)cr_root);
     }
   }
 }

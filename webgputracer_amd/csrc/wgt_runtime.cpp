@@ -128,8 +128,8 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.W = W;
   fr.H = H;
   fr.kernel = env_u32("WGT_KERNEL", 2);
-  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 24);
-  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 8);
+  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 16);  // swept on the persistent BVH4 kernel
+  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 14);
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
   fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
@@ -166,6 +166,12 @@ void fill_stats(const unsigned long long* c, wgt_stats* s) {
   s->trav_lane_steps = c[CNT_TRAV_LANE];
   s->cyc_service = c[CNT_CYC_SERVICE];
   s->cyc_trav = c[CNT_CYC_TRAV];
+  s->cyc_refill = c[CNT_CYC_REFILL];
+  s->cyc_finalise = c[CNT_CYC_FINALISE];
+  s->cyc_shade = c[CNT_CYC_SHADE];
+  s->cyc_camera = c[CNT_CYC_CAMERA];
+  s->cyc_quads = c[CNT_CYC_QUADS];
+  s->cyc_root = c[CNT_CYC_ROOT];
 }
 
 
