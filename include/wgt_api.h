@@ -170,6 +170,15 @@ int wgt_render_tile(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint3
                     uint32_t x0, uint32_t y0, uint32_t tw, uint32_t th, uint8_t *rgba8_out,
                     float *rgba32f_out, uint32_t *hit_id_out, wgt_stats *stats);
 
+/* Synchronous multi-frame render (replaces Renderer::OnCompute's frame loop,
+ * render.cpp:430-449, for a static scene): n_frames whole W x H frames, frame j
+ * with seed seeds[j], in ONE launch (the persistent kernel's end-of-launch drain
+ * is paid once per batch).  rgba8_out: n_frames x H x W x 4 bytes, frame after
+ * frame.  Frame j equals wgt_render_tile of the full frame with cam->seed =
+ * seeds[j], bit for bit. */
+int wgt_render_frames(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint32_t H,
+                      const uint32_t *seeds, uint32_t n_frames, uint8_t *rgba8_out, wgt_stats *stats);
+
 /* Tile-list launch with DEVICE buffers: n_tiles tiles of tw x th (d_tiles: device
  * array of wgt_tile) written compactly, tile after tile (out[(t*th + ly)*tw + lx]).
  * cam->seed is ignored (per-tile seeds).  Asynchronous for megakernel scenes; for

@@ -295,3 +295,17 @@ def test_mesh_tiles_reassemble_full_frame(ctx, wgt, bunny):
             tw, th = min(12, W - x0), min(12, H - y0)
             out[y0:y0 + th, x0:x0 + tw] = ctx.render_tile(cam, W, H, x0, y0, tw, th)["f32"]
     assert np.array_equal(out.view(np.uint32), full.view(np.uint32))
+
+
+def test_frame_batch_equals_single_frames(ctx, wgt, bunny):
+    """C5 launcher: a batch of whole frames in one tile-list launch (seed = frame)
+    equals each frame rendered alone with camera.seed = frame, bit for bit."""
+    from webgputracer_amd.frames import FrameRenderer
+
+    (L, Q, S, T), _ = bunny
+    ctx.upload_scene(L, Q, S, T)
+    W, H, spp = 48, 27, 4
+    imgs = FrameRenderer(ctx, W, H, spp).render([7, 8, 9])
+    for f in (7, 8, 9):
+        single = ctx.render_tile(wgt.camera_param(W / H, spp, f), W, H, want=("u8",))["u8"]
+        assert np.array_equal(imgs[f], single), f

@@ -63,7 +63,7 @@ EXPORTS = [
     "wgt_upload_scene", "wgt_scene_info_get", "wgt_render_tile", "wgt_render_tiles_async",
     "wgt_render_tiles_stats", "wgt_render_tiles_profile", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_stream",
     "wgt_scene_cornell", "wgt_make_triangles", "wgt_load_obj", "wgt_procedural_mesh",
-    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build",
+    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build", "wgt_render_frames",
 ]
 
 _lib = None
@@ -107,6 +107,7 @@ def lib():
         "wgt_write_obj": (I, [ctypes.c_char_p, P, U32]),
         "wgt_write_png": (I, [ctypes.c_char_p, P, U32, U32]),
         "wgt_bvh_build": (I, [P, U32, P, U32, P, ctypes.POINTER(WgtSceneInfo)]),
+        "wgt_render_frames": (I, [P, P, U32, U32, P, U32, P, P]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("WGT_LIB_PATH") and not hasattr(L, name):

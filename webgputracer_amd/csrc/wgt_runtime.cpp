@@ -533,6 +533,43 @@ int wgt_render_tiles_profile(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t
   return WGT_OK;
 }
 
+int wgt_render_frames(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H,
+                      const uint32_t* seeds, uint32_t n_frames, uint8_t* rgba8_out, wgt_stats* stats) {
+  int rc = check_render_args(ctx, cam, W, H, W, H);
+  if (rc) return rc;
+  if (n_frames == 0) return WGT_OK;
+  if (!seeds || !rgba8_out) return fail(ctx, WGT_E_INVALID, "null seeds or output");
+  const size_t npx = (size_t)W * H;
+  if (npx * n_frames > 0xffffffffull / 4) return fail(ctx, WGT_E_INVALID, "batch too large");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  // one full-frame tile per frame: the compact tile output is frame after frame
+  std::vector<wgt_tile> tl(n_frames);
+  for (uint32_t j = 0; j < n_frames; ++j) tl[j] = wgt_tile{0u, 0u, seeds[j], j};
+  if ((rc = ensure(ctx, ctx->tiles, n_frames * sizeof(wgt_tile)))) return rc;
+  if ((rc = ensure(ctx, ctx->out8, npx * n_frames * 4))) return rc;
+  WGT_HIP(ctx, hipMemcpyAsync(ctx->tiles.p, tl.data(), n_frames * sizeof(wgt_tile), hipMemcpyHostToDevice,
+                              ctx->stream));
+  DevFrame fr = make_frame(*cam, W, H);
+  fr.tw = W;
+  fr.th = H;
+  fr.n_tiles = n_frames;
+  FrameTiming timing;
+  if ((rc = render_frame(ctx, fr, (const wgt_tile*)ctx->tiles.p, (uchar4*)ctx->out8.p, nullptr, nullptr, nullptr,
+                         ctx->stream, stats ? &timing : nullptr)))
+    return rc;
+  WGT_HIP(ctx, hipMemcpyAsync(rgba8_out, ctx->out8.p, npx * n_frames * 4, hipMemcpyDeviceToHost, ctx->stream));
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (stats) {
+    rc = wgt_render_tiles_stats(ctx, cam, W, H, W, H, (const wgt_tile*)ctx->tiles.p, n_frames, stats);
+    if (rc) return rc;
+    stats->kernel_ms = timing.total_ms;
+    stats->trace_ms = timing.trace_ms;
+    stats->shade_ms = timing.shade_ms;
+    stats->iterations = timing.iterations;
+  }
+  return WGT_OK;
+}
+
 int wgt_render_tile(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H, uint32_t x0,
                     uint32_t y0, uint32_t tw, uint32_t th, uint8_t* rgba8_out, float* rgba32f_out,
                     uint32_t* hit_id_out, wgt_stats* stats) {

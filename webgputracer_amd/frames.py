@@ -1,0 +1,96 @@
+"""Multi-frame launcher (BASELINE config C5): a frame range
+rendered by one process per GPU, frames dealt round-robin, no collective.
+
+Replaces the reference's machine split (settings/run.py:11-24: frames 1-320 on
+one host, 321-600 on another, each running `WebGPUTracer --frame s e`,
+main.cpp:17-33) inside one node: rank r of N renders the frames f with
+(f - start) % N == r.  The camera is static (Camera::Update ignores t,
+camera.cpp:64-70), so frames differ only by their seed: seed = frame index
+(the reference draws std::random_device, util.h:43-47).
+
+Frames are rendered B per launch (wgt_render_frames: one full-frame tile per
+frame, each with its frame's seed), so the persistent kernel's end-of-launch
+drain is paid once per B frames instead of once per frame.  Every frame is
+bit-identical to a single-frame render.
+
+  python -m webgputracer_amd.frames --frame 1 600 --spp 64 --scene bunny --batch 4 --out out/
+  python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+      -m webgputracer_amd.frames --frame 1 600 --spp 64 --batch 4 --out out/
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+
+from .tracer import Context, camera_param, cornell_scene, mesh_scene, write_png
+
+
+def frames_of_rank(start: int, end: int, rank: int, world: int):
+    """Frames [start, end] of `rank`: round-robin, as even as the range allows."""
+    if end < start:
+        return []
+    return [f for f in range(start, end + 1) if (f - start) % world == rank]
+
+
+def batches(frames, batch: int):
+    return [frames[i:i + batch] for i in range(0, len(frames), max(batch, 1))]
+
+
+class FrameRenderer:
+    """Renders batches of whole frames on one GPU (wgt_render_frames: one launch per
+    batch, host output)."""
+
+    def __init__(self, ctx: Context, W: int, H: int, spp: int):
+        self.ctx, self.W, self.H, self.spp = ctx, W, H, spp
+        self.cam = camera_param(W / H, spp, 0)  # per-frame seeds override cam.seed
+
+    def render(self, frames):
+        """{frame: (H, W, 4) uint8} for the batch `frames`, seed = frame index."""
+        out = self.ctx.render_frames(self.cam, self.W, self.H, np.asarray(frames, np.uint32))
+        return {f: out[j] for j, f in enumerate(frames)}
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.split("\n\n")[0])
+    ap.add_argument("--frame", nargs=2, type=int, default=[1, 1], metavar=("START", "END"))
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--scene", default="bunny", help="bunny | sponza | cornell | obj:<path>")
+    ap.add_argument("--batch", type=int, default=4, help="frames per launch")
+    ap.add_argument("--out", default=None, help="directory for NNN.png (none: render only)")
+    a = ap.parse_args(argv)
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.scene == "cornell":
+        scene = cornell_scene()
+    elif a.scene.startswith("obj:"):
+        scene = mesh_scene("bunny", obj_path=a.scene[4:])
+    else:
+        scene = mesh_scene(a.scene)
+    ctx = Context(local)
+    ctx.upload_scene(*scene)
+    fr = FrameRenderer(ctx, a.width, a.height, a.spp)
+    mine = frames_of_rank(a.frame[0], a.frame[1], rank, world)
+    if a.out:
+        os.makedirs(a.out, exist_ok=True)
+    t0 = time.perf_counter()
+    for b in batches(mine, a.batch):
+        imgs = fr.render(b)
+        if a.out:
+            for f in b:
+                write_png(os.path.join(a.out, f"{f:03d}.png"), imgs[f])  # render.cpp:494-497
+    dt = time.perf_counter() - t0
+    print(json.dumps({"rank": rank, "world": world, "frames": len(mine), "batch": a.batch, "seconds": round(dt, 3),
+                      "frames_per_s": round(len(mine) / dt, 3) if dt > 0 else None}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

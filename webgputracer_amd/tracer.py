@@ -172,6 +172,16 @@ class Context:
                                             ctypes.byref(st) if st is not None else None))
         return {"u8": u8, "f32": f32, "hit": hit, "stats": st.as_dict() if st is not None else None}
 
+    def render_frames(self, cam, W, H, seeds, stats=False):
+        """n whole frames in one launch (wgt_render_frames): (n, H, W, 4) uint8 (+ stats)."""
+        seeds = np.ascontiguousarray(seeds, np.uint32)
+        out = np.zeros((len(seeds), H, W, 4), np.uint8)
+        st = WgtStats() if stats else None
+        cam = np.ascontiguousarray(cam, CAMERA_DTYPE)
+        self._check(self._L.wgt_render_frames(self.h, ptr(cam), W, H, ptr(seeds), len(seeds), ptr(out),
+                                              ctypes.byref(st) if st is not None else None))
+        return (out, st.as_dict()) if stats else out
+
     def render_tiles_async(self, cam, W, H, tw, th, d_tiles, n_tiles, d_u8=0, d_f32=0, d_hit=0, stream=0):
         """Device-pointer launch (ints are raw device addresses, 0 = NULL)."""
         cam = np.ascontiguousarray(cam, CAMERA_DTYPE)
