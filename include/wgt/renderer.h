@@ -25,6 +25,7 @@ struct RendererConfig {
   std::string out_dir = ".";
   bool fixed_seed = false;        // seed = frame index instead of RandSeed()
   bool write_png = true;
+  uint32_t batch = 1;             // frames per launch in OnCompute (wgt_render_frames); 1 = reference loop
 };
 
 class Renderer {
@@ -36,6 +37,8 @@ class Renderer {
   bool OnInit(bool hasWindow);                              // render.cpp:12-45
   bool OnCompute(uint32_t start_frame, uint32_t end_frame); // render.cpp:430-449
   bool OnRender(uint32_t frame);                            // render.cpp:451-511
+  // OnRender for frames [first, first + n) in one launch (frame f -> "fff.png")
+  bool OnRenderBatch(uint32_t first, uint32_t n);
   void OnFinish();                                          // render.cpp:599-650
   bool IsRunning() { return false; }  // no window on the GPU box
 

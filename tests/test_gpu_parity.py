@@ -309,3 +309,25 @@ def test_frame_batch_equals_single_frames(ctx, wgt, bunny):
     for f in (7, 8, 9):
         single = ctx.render_tile(wgt.camera_param(W / H, spp, f), W, H, want=("u8",))["u8"]
         assert np.array_equal(imgs[f], single), f
+
+
+def test_cli_batched_frames_equal_reference_loop(tmp_path):
+    """wgt_tracer --batch 3 (Renderer::OnRenderBatch, one launch for three frames)
+    writes the same 000.png..002.png as the reference-style one-frame loop."""
+    import os
+    import subprocess
+
+    from PIL import Image
+
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "webgputracer_amd", "wgt_tracer")
+    outs = {}
+    for b in (1, 3):
+        d = tmp_path / f"b{b}"
+        d.mkdir()
+        r = subprocess.run([exe, "--frame", "1", "3", "--width", "40", "--height", "24", "--spp", "4", "--scene",
+                            "bunny", "--fixed-seed", "--batch", str(b), "--out", str(d)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr
+        outs[b] = [np.asarray(Image.open(d / f"{f:03d}.png").convert("RGBA")) for f in range(3)]
+    for f in range(3):
+        assert np.array_equal(outs[1][f], outs[3][f]), f

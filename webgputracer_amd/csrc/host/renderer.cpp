@@ -6,6 +6,7 @@
 // the same wall-clock logging (render.cpp:430-449).
 #include "../../../include/wgt/renderer.h"
 
+#include <algorithm>
 #include <chrono>
 #include <iomanip>
 #include <iostream>
@@ -51,7 +52,12 @@ bool Renderer::OnCompute(uint32_t start_frame, uint32_t end_frame) {
   std::cout << "[WebGPUTracer] Running compute pass ..." << std::endl;
   auto start = std::chrono::system_clock::now();
   bool success = false;
-  for (uint32_t i = start_frame - 1; i < end_frame; ++i) success = OnRender(i);
+  if (cfg_.batch <= 1) {
+    for (uint32_t i = start_frame - 1; i < end_frame; ++i) success = OnRender(i);
+  } else {
+    for (uint32_t i = start_frame - 1; i < end_frame; i += cfg_.batch)
+      success = OnRenderBatch(i, std::min(cfg_.batch, end_frame - i));
+  }
   auto end = std::chrono::system_clock::now();
   double elapsed = (double)std::chrono::duration_cast<std::chrono::milliseconds>(end - start).count();
   std::cout << "[WebGPUTracer] Finished: " << elapsed * 0.001 << "(sec)s" << std::endl;
@@ -83,6 +89,40 @@ bool Renderer::OnRender(uint32_t frame) {
   auto end = std::chrono::system_clock::now();
   double elapsed = (double)std::chrono::duration_cast<std::chrono::milliseconds>(end - start).count();
   std::cout << "[" << sout.str() << "]: " << elapsed * 0.001 << "(sec)s" << std::endl;
+  return true;
+}
+
+bool Renderer::OnRenderBatch(uint32_t first, uint32_t n) {
+  auto start = std::chrono::system_clock::now();
+  float aspect = (float)cfg_.width / (float)cfg_.height;
+  std::vector<uint32_t> seeds(n);
+  for (uint32_t j = 0; j < n; ++j) {  // the seed OnRender would use for frame first + j
+    if (cfg_.fixed_seed) camera_.SetSeed(first + j);
+    camera_.Update((float)(first + j) / (float)cfg_.max_frame, aspect);
+    seeds[j] = camera_.GetParam().seed;
+  }
+  const size_t frame_bytes = (size_t)cfg_.width * cfg_.height * 4;
+  std::vector<uint8_t> images(frame_bytes * n);
+  if (wgt_render_frames(ctx_, &camera_.GetParam(), cfg_.width, cfg_.height, seeds.data(), n, images.data(),
+                        nullptr) != WGT_OK) {
+    std::cerr << "[WebGPUTracer] render failed: " << wgt_last_error(ctx_) << std::endl;
+    return false;
+  }
+  for (uint32_t j = 0; j < n; ++j) {
+    std::ostringstream sout;
+    sout << std::setw(3) << std::setfill('0') << first + j;
+    if (cfg_.write_png) {
+      std::string output_file = cfg_.out_dir + "/" + sout.str() + ".png";
+      if (wgt_write_png(output_file.c_str(), images.data() + frame_bytes * j, cfg_.width, cfg_.height) != WGT_OK) {
+        std::cerr << "[WebGPUTracer] Image output failed." << std::endl;
+        return false;
+      }
+    }
+  }
+  image_.assign(images.end() - frame_bytes, images.end());
+  auto end = std::chrono::system_clock::now();
+  double elapsed = (double)std::chrono::duration_cast<std::chrono::milliseconds>(end - start).count();
+  std::cout << "[" << first << "-" << first + n - 1 << "]: " << elapsed * 0.001 << "(sec)s" << std::endl;
   return true;
 }
 

@@ -1,7 +1,7 @@
 // main.cpp — CLI mirroring src/main.cpp of the reference:
 //   wgt_tracer [--frame start end] [--width W] [--height H] [--spp N]
 //              [--scene cornell|bunny|sponza|obj:<path>] [--device D] [--out DIR]
-//              [--fixed-seed] [--no-png]
+//              [--fixed-seed] [--no-png] [--batch B]
 // The reference parses only `--frame s e` (main.cpp:21-26) with W=H=512,
 // SPP=1000 compiled in (renderer.h:53-56); those stay the defaults.
 #include <cstdlib>
@@ -30,6 +30,7 @@ int main(int argc, char* argv[]) {
     else if (!std::strcmp(argv[i], "--out")) { need(1); cfg.out_dir = argv[++i]; }
     else if (!std::strcmp(argv[i], "--fixed-seed")) { cfg.fixed_seed = true; }
     else if (!std::strcmp(argv[i], "--no-png")) { cfg.write_png = false; }
+    else if (!std::strcmp(argv[i], "--batch")) { need(1); cfg.batch = (uint32_t)atoi(argv[++i]); }
     else { std::cerr << "[WebGPUTracer] unknown option " << argv[i] << std::endl; return 2; }
   }
   if (start_frame < 1 || end_frame < start_frame) {
