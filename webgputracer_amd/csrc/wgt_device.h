@@ -269,6 +269,102 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
   return false;
 }
 
+// ---------------------------------------------------------------------------
+// Speculative two-mode traversal (k_render_ps).  A wave step is uniformly a
+// NODE step (lanes with an internal node to visit) or a TRIANGLE step (lanes
+// with a pending leaf), so a step issues one of the two code paths instead of
+// both.  A lane that reaches a leaf parks it as its pending leaf and keeps
+// descending (speculation, after Aila & Laine's speculative while-while); a
+// second leaf found meanwhile waits on the stack (one entry beyond the
+// builder's bound: DevScene::stack includes it).  Culling with a not yet
+// updated best t is only less tight, never wrong: the closest hit is a minimum
+// over (t, index) of every triangle whose boxes the ray enters.
+//
+// Lane state after every step: an internal node in t.ref, or kNoRef with a
+// pending leaf (lf < le), or done (kNoRef, no pending leaf, empty stack).
+constexpr int kNoRef = 0x7fffffff;
+
+// Place `cand` (a child ref, or kNoRef = take the next stack entry).
+__device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int cand, int* __restrict__ lds) {
+#pragma unroll
+  for (int it = 0; it < 3; ++it) {
+    if (cand == kNoRef) {
+      if (t.sp == 0 || ++t.iters > sc.max_iters) break;
+      --t.sp;
+      cand = lds[t.sp * kBlock];
+    }
+    if (cand >= 0) {
+      t.ref = cand;
+      return;
+    }
+    if (t.lf >= t.le) {  // no pending leaf: this one becomes it; keep looking for a node
+      t.lf = leaf_first(cand);
+      t.le = t.lf + leaf_count(cand);
+      cand = kNoRef;
+      continue;
+    }
+    lds[t.sp * kBlock] = cand;  // a second leaf waits on the stack
+    ++t.sp;
+    break;
+  }
+  t.ref = kNoRef;
+}
+
+__device__ __forceinline__ bool trav_done(const Trav& t) { return t.ref == kNoRef && t.lf >= t.le && t.sp == 0; }
+
+// Visit t.ref: sort the hit children, push all but the nearest, place the nearest.
+template <bool STATS>
+__device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, int* __restrict__ lds, TravStats& st) {
+  const float4* __restrict__ n = sc.nodes + 8 * t.ref;
+  const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
+  const float4 rf = n[6];
+  if (STATS) st.nodes++;
+  int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z),
+      r3 = __float_as_int(rf.w);
+  uint32_t k0 = child_key(t, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, 0u);
+  uint32_t k1 = child_key(t, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, 1u);
+  uint32_t k2 = child_key(t, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, 2u);
+  uint32_t k3 = child_key(t, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, 3u);
+  cas(k0, r0, k1, r1);
+  cas(k2, r2, k3, r3);
+  cas(k0, r0, k2, r2);
+  cas(k1, r1, k3, r3);
+  cas(k1, r1, k2, r2);
+  lds[t.sp * kBlock] = r3;
+  t.sp += k3 != kMissKey ? 1 : 0;
+  lds[t.sp * kBlock] = r2;
+  t.sp += k2 != kMissKey ? 1 : 0;
+  lds[t.sp * kBlock] = r1;
+  t.sp += k1 != kMissKey ? 1 : 0;
+  trav_resolve(sc, t, k0 != kMissKey ? r0 : kNoRef, lds);
+}
+
+// Test the next triangle of the pending leaf; a lane without a node to visit
+// takes the next stack entry once its leaf is done.
+template <bool STATS>
+__device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, int* __restrict__ lds,
+                                         TravStats& st) {
+  const float4* __restrict__ tp = sc.tris + 4 * t.lf;
+  const float4 A = tp[0], B = tp[1], C = tp[2];
+  if (STATS) st.tris++;
+  float tt;
+  if (mt_test(o, d, xyz(A), xyz(B), xyz(C), tt)) {
+    const uint32_t idx = __float_as_uint(A.w);
+    if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
+      const float4 D = tp[3];
+      float bn, bf;
+      slab(t.ot, t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
+      if (bn <= tt && tt <= bf) {
+        t.bt = tt;
+        t.bi = idx;
+        t.found = true;
+      }
+    }
+  }
+  ++t.lf;
+  if (t.lf >= t.le && t.ref == kNoRef) trav_resolve(sc, t, kNoRef, lds);
+}
+
 // Merge the triangle result into the quad hit, then scan the spheres: the end of
 // sample_hit (path_tracer.wgsl:305-309) with triangles between quads and spheres.
 __device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const Trav& t, Hit& h) {

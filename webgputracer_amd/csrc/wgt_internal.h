@@ -60,6 +60,9 @@ struct DevFrame {
   // once <= ps_to_service lanes still traverse.
   uint32_t kernel;  // scenes with triangles: 0 = wavefront, 1 = simple, 2 = phase-split (default)
   uint32_t ps_to_trav, ps_to_service;
+  // speculative traversal: a triangle step runs when lanes with a pending leaf
+  // number >= tri_ratio % of the lanes with a node to visit
+  uint32_t tri_ratio;
   // wavefront: rays a slot may start per shade launch, slots per trace wave,
   // idle lanes that trigger a refill from the wave's ray list
   uint32_t wf_rays, wf_chunk, wf_refill;

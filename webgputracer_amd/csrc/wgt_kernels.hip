@@ -227,9 +227,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           if (COST) work += kCostService;
           // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
-          bool done_root = false;
-          WGT_REGION(cr_root, done_root = trav_step<STATS>(sc, ro, rd, t, lds, st));
-          if (done_root) pending = true;
+          WGT_REGION(cr_root, node_step<STATS>(sc, t, lds, st));
+          if (trav_done(t)) pending = true;
           else trav = true;
           break;
         }
@@ -244,8 +243,21 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
     if (__ballot(have || !exhausted) == 0ull) break;
     // --------------------------------------------------------- traversal phase
     for (;;) {
-      if (COST && trav) ++work;
-      if (trav && trav_step<STATS>(sc, ro, rd, t, lds, st)) {
+      // one uniform mode per step: triangle steps once enough lanes hold a
+      // pending leaf (weighted by the two steps' costs), else node steps
+      const bool can_node = trav && t.ref != kNoRef;
+      const bool can_tri = trav && t.lf < t.le;
+      const uint32_t nn = (uint32_t)__popcll(__ballot(can_node));
+      const uint32_t nl = (uint32_t)__popcll(__ballot(can_tri));
+      const bool tri_mode = nn == 0 || nl * 100u >= nn * fr.tri_ratio;
+      if (STATS && (tri_mode ? can_tri : can_node)) simt_count(st.wave_steps, st.lane_steps);
+      if (COST && (tri_mode ? can_tri : can_node)) ++work;
+      if (tri_mode) {
+        if (can_tri) tri_step<STATS>(sc, ro, rd, t, lds, st);
+      } else {
+        if (can_node) node_step<STATS>(sc, t, lds, st);
+      }
+      if (trav && trav_done(t)) {
         trav = false;
         pending = true;
       }

@@ -130,6 +130,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.kernel = env_u32("WGT_KERNEL", 2);
   fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 16);  // swept on the persistent BVH4 kernel
   fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 14);
+  fr.tri_ratio = env_u32("WGT_TRI_RATIO", 100);
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
   fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
@@ -435,7 +436,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const f3 lu = f3{lights[0].up[0], lights[0].up[1], lights[0].up[2]};
   sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
   sc.max_iters = 4u * bvh.n_nodes + 8u;
-  sc.stack = bvh.stack_need > 0 ? bvh.stack_need : 1u;
+  // + 1: the speculative traversal parks a second leaf on the stack (wgt_device.h)
+  sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
   WGT_HIP(ctx, ps_resident_waves(sc, ctx->device, ctx->ps_resident));
 
   wgt_scene_info& in = ctx->info;
@@ -451,7 +453,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   in.device_bytes = total;
   in.sah_cost = bvh.sah_cost;
   in.bvh_width = n_tris ? (uint32_t)kBvhWidth : 0u;
-  in.bvh_stack = n_tris ? sc.stack : 0u;
+  in.bvh_stack = n_tris ? std::max(bvh.stack_need, 1u) : 0u;
   in.bvh2_nodes = bvh.n_nodes2;
   in.bvh2_depth = bvh.depth2;
   ctx->has_scene = true;
