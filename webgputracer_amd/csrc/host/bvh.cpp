@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 
@@ -54,8 +55,19 @@ uint32_t MedianDepth(uint32_t count) {
   }
   return d;
 }
-constexpr double kCostTrav = 1.0;
+// SAH costs of a BVH2 node visit and a triangle test, and the largest leaf the
+// SAH may choose (<= kLeafMax, the encoding's limit).  WGT_SAH_TRAV / WGT_SAH_LEAF
+// override them for tuning sweeps; the defaults are the measured best.
 constexpr double kCostTri = 1.0;
+double SahTravCost() {
+  const char* v = std::getenv("WGT_SAH_TRAV");
+  return v && *v ? std::atof(v) : 1.0;
+}
+uint32_t SahLeafMax() {
+  const char* v = std::getenv("WGT_SAH_LEAF");
+  const int n = v && *v ? std::atoi(v) : kLeafMax;
+  return (uint32_t)std::max(1, std::min(n, kLeafMax));
+}
 
 class Builder {
  public:
@@ -124,9 +136,9 @@ class Builder {
           }
         }
       }
-      const double split_cost = kCostTrav + kCostTri * (parea > 0 ? best / parea : 0.0);
+      const double split_cost = cost_trav_ + kCostTri * (parea > 0 ? best / parea : 0.0);
       const double leaf_cost = kCostTri * count;
-      if (best_axis >= 0 && !(count <= (uint32_t)kLeafMax && leaf_cost <= split_cost)) {
+      if (best_axis >= 0 && !(count <= sah_leaf_ && leaf_cost <= split_cost)) {
         const float ext = cb.hi[best_axis] - cb.lo[best_axis];
         const double scale = kBins / (double)ext;
         auto it = std::partition(prims_.begin() + begin, prims_.begin() + end, [&](const Prim& p) {
@@ -159,7 +171,7 @@ class Builder {
     const int rl = Build(begin, mid, depth + 1, bl);
     const int rr = Build(mid, end, depth + 1, br);
     WriteNode(id, bl, rl, br, rr);
-    out_.sah_cost += kCostTrav * box.area();
+    out_.sah_cost += cost_trav_ * box.area();
     return (int)id;
   }
 
@@ -186,6 +198,8 @@ class Builder {
   BvhOut& out_;
   std::vector<float>& nodes_;
   uint32_t limit_;
+  double cost_trav_ = SahTravCost();
+  uint32_t sah_leaf_ = SahLeafMax();
 };
 
 
