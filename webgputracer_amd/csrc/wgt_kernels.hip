@@ -90,7 +90,8 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
 // slots are one 8x8 pixel block.  Each pixel's result depends only on its
 // coordinates and seed: which lane or wave computes it does not change a bit.
 // COST: the 1-spp pre-pass: no output, each finished pixel adds its work units
-// (kCostService per ray started + 1 per traversal step) to fr.cost[its block].
+// (kCostService per ray started + 1 per traversal step) to fr.cost[its block];
+// it renders the 16 pixels at even (x, y) of each 8x8 block.
 constexpr uint32_t kCostService = 7;  // a service iteration ~ 7 traversal steps (profiles/)
 // STATS: wave cycles per service-phase region (s_memtime; the regions run in
 // divergent code, so each adds the wave's time spent issuing or waiting in it).
@@ -158,8 +159,11 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             if (slot >= n_slots) {
               exhausted = true;
             } else {
-              const uint32_t b = fr.perm ? fr.perm[slot >> 6] : (slot >> 6);
-              if (slot_setup(fr, tiles, b, slot & 63u, tile, lx, ly, px)) {
+              // COST pre-pass: 16 slots per block, the pixels at even (x, y) of the 8x8 block
+              const uint32_t sb = COST ? (slot >> 4) : (slot >> 6);
+              const uint32_t sl = COST ? (((slot & 3u) << 1) | (((slot >> 2) & 3u) << 4)) : (slot & 63u);
+              const uint32_t b = fr.perm ? fr.perm[sb] : sb;
+              if (slot_setup(fr, tiles, b, sl, tile, lx, ly, px)) {
                 have = true;
                 depth = 0;
                 pblock = b;
@@ -359,6 +363,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       fc.recip_sqrt_spp = 1.0f / (float)fc.sqrt_spp;
       fc.fspp = (float)(fc.sqrt_spp * fc.sqrt_spp);
       fc.cost = (uint32_t*)((char*)ws + 256);
+      fc.n_slots = nb * 16u;  // a quarter of each block's pixels estimate its cost
       k_render_ps<false, true><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
       k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb);
       f.perm = fc.cost + nb;

@@ -134,7 +134,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
   fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
-  fr.pq_refill = env_u32("WGT_PQ_REFILL", 8);
+  fr.pq_refill = env_u32("WGT_PQ_REFILL", 4);  // sweep: 2-4 best (profiles/sweeps)
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   if (fr.pq_refill < 1) fr.pq_refill = 1;
