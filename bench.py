@@ -54,6 +54,10 @@ def parse():
     p.add_argument("--cpu-rows", type=int, default=0, help="rows in the CPU-baseline sample (0 = auto)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on fewer GPUs")
+    p.add_argument("--check", action="store_true",
+                   help="rank 0 compares the assembled frames with single-launch renders (bit-exact)")
     return p.parse_args()
 
 
@@ -107,12 +111,16 @@ def main():
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; rehearsals with more ranks than GPUs share devices (gloo only)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
@@ -146,14 +154,14 @@ def main():
                                stream=stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
-        bufs = wdist.gather_tiles(out, rank, world, dist)
+        bufs = wdist.gather_tiles(out if args.dist_backend == "nccl" else out.cpu(), rank, world, dist)
         if rank == 0:
             if world == 1:
                 img = wdist.assemble(tiles, out, W, H, T, [0], xp=torch)
             else:
                 all_tiles = [wdist.pad_tiles(wdist.shard_tiles(W, H, T, frames, r, world), n_max)
                              for r in range(world)]
-                img = wdist.assemble(np.concatenate(all_tiles), torch.cat(bufs), W, H, T,
+                img = wdist.assemble(np.concatenate(all_tiles), torch.cat(bufs).to(dev), W, H, T,
                                      [f for f, _ in frames], xp=torch)
             return img
         return None
@@ -165,8 +173,9 @@ def main():
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     t0 = time.perf_counter()
+    img = None
     for k in range(args.steps):
-        step(evs[k])
+        img = step(evs[k])
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
@@ -177,8 +186,14 @@ def main():
                      st["tri_tests"], kern_ms], np.float64)
     simt = {"path_loop": st["loop_lane_iters"] / max(64 * st["loop_wave_iters"], 1),
             "bvh_loop": st["trav_lane_steps"] / max(64 * st["trav_wave_steps"], 1)}
+    check = None
+    if args.check and rank == 0 and img is not None:  # outside the timed region
+        check = True
+        for fid, seed in frames:
+            ref = ctx.render_frames(w.camera_param(W / H, spp, 0), W, H, np.array([seed], np.uint32))[0]
+            check &= bool(np.array_equal(img[fid].cpu().numpy(), ref))
     if world > 1:
-        tm = torch.tensor(mine, device=dev)
+        tm = torch.tensor(mine, device=dev if args.dist_backend == "nccl" else "cpu")
         allv = [torch.zeros_like(tm) for _ in range(world)]
         dist.all_gather(allv, tm)
         allv = np.stack([a.cpu().numpy() for a in allv])
@@ -221,7 +236,8 @@ def main():
                     if args.scene != "cornell" else "synthetic: reference Cornell box",
             "config": {"workload": f"{args.scene}-{W}x{H}-{spp}spp", "width": W, "height": H, "spp": spp,
                        "triangles": n_tris, "bvh_nodes": info["bvh_nodes"], "tile": T,
-                       "frames_per_step": world, "parallelism": f"tiles{world}+rccl-gather"},
+                       "frames_per_step": world,
+                       "parallelism": f"tiles{world}+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}-gather"},
             "samples_per_s": round(samples / max_t, 1),
             "reference_queries_per_s": round(queries / max_t, 1),
             "kernel_ms": round(kern_ms, 3),
@@ -233,6 +249,8 @@ def main():
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
             "cpu_baseline": base,
         }
+        if check is not None:
+            line["check_frames_bit_exact"] = check
         print(json.dumps(line), flush=True)
     ctx.close()
     if world > 1:
