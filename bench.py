@@ -147,6 +147,15 @@ def main():
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
 
+    # rank 0 assembles the step's frames with one gather op (index built once, here)
+    frame_ids = [f for f, _ in frames]
+    if world == 1:
+        layout = tiles
+    else:
+        layout = np.concatenate([wdist.pad_tiles(wdist.shard_tiles(W, H, T, frames, r, world), n_max)
+                                 for r in range(world)])
+    asm_idx = torch.from_numpy(wdist.assemble_index(layout, W, H, T, frame_ids)).to(dev) if rank == 0 else None
+
     def step(ev):
         if ev is not None:
             ev[0].record(stream)
@@ -156,14 +165,9 @@ def main():
             ev[1].record(stream)
         bufs = wdist.gather_tiles(out if args.dist_backend == "nccl" else out.cpu(), rank, world, dist)
         if rank == 0:
-            if world == 1:
-                img = wdist.assemble(tiles, out, W, H, T, [0], xp=torch)
-            else:
-                all_tiles = [wdist.pad_tiles(wdist.shard_tiles(W, H, T, frames, r, world), n_max)
-                             for r in range(world)]
-                img = wdist.assemble(np.concatenate(all_tiles), torch.cat(bufs).to(dev), W, H, T,
-                                     [f for f, _ in frames], xp=torch)
-            return img
+            data = (bufs[0] if world == 1 else torch.cat(bufs)).to(dev).reshape(-1, 4)
+            imgs = data[asm_idx]  # (frames, H, W, 4)
+            return {f: imgs[i] for i, f in enumerate(frame_ids)}
         return None
 
     for _ in range(args.warmup):

@@ -93,3 +93,23 @@ def test_gloo_world2_gather_assembles_frames(tmp_path):
     result = tmp_path / "result.txt"
     mp.start_processes(_worker, args=(2, _free_port(), str(result)), nprocs=2, join=True, start_method="spawn")
     assert result.read_text() == "ok"
+
+
+def test_assemble_index_matches_assemble():
+    """The one-op gather index used by bench.py equals the tile-by-tile assembly."""
+    import numpy as np
+
+    from webgputracer_amd import dist as wdist
+
+    W, H, T, world = 70, 45, 16, 3
+    frames = [(j, 100 + j) for j in range(world)]
+    n_max = wdist.max_tiles_per_rank(W, H, T, world, world)
+    layout = np.concatenate([wdist.pad_tiles(wdist.shard_tiles(W, H, T, frames, r, world), n_max)
+                             for r in range(world)])
+    rng = np.random.default_rng(0)
+    data = rng.integers(0, 255, (len(layout), T, T, 4), dtype=np.uint8)
+    ref = wdist.assemble(layout, data, W, H, T, [f for f, _ in frames])
+    idx = wdist.assemble_index(layout, W, H, T, [f for f, _ in frames])
+    got = data.reshape(-1, 4)[idx]
+    for i, (f, _) in enumerate(frames):
+        assert np.array_equal(got[i], ref[f])

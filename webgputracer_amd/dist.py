@@ -65,6 +65,24 @@ def assemble(tiles: np.ndarray, data, W: int, H: int, T: int, frame_ids, xp=np):
     return frames
 
 
+def assemble_index(tiles: np.ndarray, W: int, H: int, T: int, frame_ids):
+    """Gather index for assembling frames in one indexing op: for the tile list
+    `tiles` (compact buffer data[k] of shape (T, T, C), flattened to rows of C),
+    returns idx of shape (len(frame_ids), H, W) with frames[i] = data.reshape(-1, C)[idx[i]].
+    Same result as assemble(); computed once on the host, used every step."""
+    fpos = {int(f): i for i, f in enumerate(frame_ids)}
+    idx = np.zeros((len(frame_ids), H, W), np.int64)
+    ly, lx = np.meshgrid(np.arange(T), np.arange(T), indexing="ij")
+    for k in range(len(tiles)):
+        fid = int(tiles["frame"][k])
+        if fid not in fpos:
+            continue
+        x0, y0 = int(tiles["x0"][k]), int(tiles["y0"][k])
+        w, h = min(T, W - x0), min(T, H - y0)
+        idx[fpos[fid], y0:y0 + h, x0:x0 + w] = (k * T + ly[:h, :w]) * T + lx[:h, :w]
+    return idx
+
+
 def pad_tiles(tiles: np.ndarray, n: int):
     """Pad a tile list to n entries (pad tiles have frame = 0xffffffff and are ignored by assemble)."""
     if len(tiles) >= n:
