@@ -349,6 +349,21 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
     return false;
   }
   out.n_nodes = (uint32_t)(out.nodes.size() / kNode4Floats);
+  // The device traversal has no iteration cap: it terminates because every
+  // internal ref points forward (preorder), so no node is visited twice.
+  for (uint32_t i = 0; i < out.n_nodes; ++i) {
+    for (int s = 0; s < 4; ++s) {
+      int32_t r;
+      std::memcpy(&r, &out.nodes[(size_t)i * kNode4Floats + 24 + s], 4);
+      const uint32_t u = ~(uint32_t)r;
+      const bool ok = r >= 0 ? ((uint32_t)r > i && (uint32_t)r < out.n_nodes)
+                             : ((uint64_t)(u >> 3) + (u & 7u) + 1u <= n);
+      if (!ok) {
+        err = "BuildBvh: malformed node " + std::to_string(i);
+        return false;
+      }
+    }
+  }
   out.tris.resize((size_t)n * kTriRecordFloats);
   for (uint32_t i = 0; i < n; ++i) {
     const wgt_triangle& t = tris[prims[i].idx];

@@ -147,21 +147,22 @@ struct Trav {
   int ref;          // current internal node (when no leaf is open)
   uint32_t lf, le;  // open leaf: next triangle, end
   int sp;
-  uint32_t iters;
-  bool found;
 };
+// A triangle was accepted (bi starts at kNoHit, see trav_init).
+__device__ __forceinline__ bool trav_found(const Trav& t) { return t.bi != kNoHit; }
 
 __device__ __forceinline__ void trav_init(f3 o, f3 d, bool quad_hit, float qt, Trav& t) {
   t.inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
   t.ot = slab_offset(o, t.inv);
-  // a triangle must satisfy t < t_quad to beat a quad hit (ray_dist is monotone in t)
-  t.bt = quad_hit ? qt : kRayMax;
-  t.bi = quad_hit ? 0u : kNoHit;
+  // a triangle must satisfy t < t_quad to beat a quad hit (ray_dist is monotone in
+  // t): with bi = kNoHit the rule "t < bt, or t == bt and index < bi" accepts
+  // exactly t <= bt, so bt = the float below t_quad (t_quad > 0).  A box entered
+  // at t_quad could only hold triangles with t >= t_quad, so culling it is exact.
+  t.bt = quad_hit ? __uint_as_float(__float_as_uint(qt) - 1u) : kRayMax;
+  t.bi = kNoHit;
   t.ref = 0;
   t.lf = t.le = 0;
   t.sp = 0;
-  t.iters = 0;
-  t.found = false;
 }
 
 
@@ -222,7 +223,6 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
         if (bn <= tt && tt <= bf) {
           t.bt = tt;
           t.bi = idx;
-          t.found = true;
         }
       }
     }
@@ -257,7 +257,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
     pop = k0 == kMissKey;
   }
   if (pop) {
-    if (t.sp == 0 || ++t.iters > sc.max_iters) return true;
+    if (t.sp == 0) return true;
     --t.sp;
     next = lds[t.sp * kBlock];
   }
@@ -289,7 +289,7 @@ __device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int ca
 #pragma unroll
   for (int it = 0; it < 3; ++it) {
     if (cand == kNoRef) {
-      if (t.sp == 0 || ++t.iters > sc.max_iters) break;
+      if (t.sp == 0) break;
       --t.sp;
       cand = lds[t.sp * kBlock];
     }
@@ -357,7 +357,6 @@ __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t
       if (bn <= tt && tt <= bf) {
         t.bt = tt;
         t.bi = idx;
-        t.found = true;
       }
     }
   }
@@ -369,7 +368,7 @@ __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t
 // sample_hit (path_tracer.wgsl:305-309) with triangles between quads and spheres.
 __device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const Trav& t, Hit& h) {
   const uint32_t nlq = sc.n_lights + sc.n_quads;
-  if (t.found) {
+  if (trav_found(t)) {
     const f3 pos = o + t.bt * d;
     const float ray_dist = distance(pos, o);
     if (!(ray_dist >= h.dist)) {
@@ -477,10 +476,14 @@ __device__ __forceinline__ uint8_t unorm8(float x) {
 struct Pixel {
   uint32_t x, y;
   uint32_t seed;
-  uint32_t k, si, sj;  // sample index and its (s_i, s_j)
+  uint32_t si, sj;  // the sample's (s_i, s_j); sample index = si + sj * sqrt_spp
   f3 col;
   uint32_t hit0;
 };
+// all sqrt_spp^2 samples done (sj reaches sqrt_spp; at once when spp = 0)
+__device__ __forceinline__ bool px_done(const DevFrame& fr, const Pixel& px) { return px.sj >= fr.sqrt_spp; }
+// sample 0 (the one whose first hit is the pixel's hit ID)
+__device__ __forceinline__ bool px_first(const Pixel& px) { return (px.si | px.sj) == 0u; }
 
 struct Counters {
   uint32_t q, tr, nan, lw, ll;
@@ -489,35 +492,36 @@ struct Counters {
 
 // Pixel of pixel slot (block, lane) = (slot >> 6, slot & 63): block b covers an
 // 8x8 sub-block of tile b / (sub-blocks per tile).  false if the slot is outside
-// its tile or the frame (ragged tiles).
+// its tile or the frame.  po = the pixel's offset in the tile-major output
+// ((tile * th + ly) * tw + lx; the host keeps tiles * tw * th < 2^31).
 __device__ __forceinline__ bool slot_setup(const DevFrame& fr, const wgt_tile* __restrict__ tiles,
-                                           uint32_t block, uint32_t lane, uint32_t& tile,
-                                           uint32_t& lx, uint32_t& ly, Pixel& px) {
+                                           uint32_t block, uint32_t lane, uint32_t& po, Pixel& px) {
   const uint32_t bx = (fr.tw + 7u) >> 3, by = (fr.th + 7u) >> 3;
   const uint32_t bpt = bx * by;
-  tile = block / bpt;
+  const uint32_t tile = block / bpt;
   const uint32_t rem = block - tile * bpt;
-  lx = (rem % bx) * 8u + (lane & 7u);
-  ly = (rem / bx) * 8u + (lane >> 3);
+  const uint32_t lx = (rem % bx) * 8u + (lane & 7u);
+  const uint32_t ly = (rem / bx) * 8u + (lane >> 3);
   if (tile >= fr.n_tiles || lx >= fr.tw || ly >= fr.th) return false;
   const wgt_tile td = tiles[tile];
   px.x = td.x0 + lx;
   px.y = td.y0 + ly;
   if (px.x >= fr.W || px.y >= fr.H) return false;  // path_tracer.wgsl:377
   px.seed = px.x + px.y * fr.W + td.seed * fr.W * fr.H;  // path_tracer.wgsl:378
-  px.k = px.si = px.sj = 0;
+  px.si = px.sj = 0;
   px.col = f3{0.0f, 0.0f, 0.0f};
   px.hit0 = kNoHit;
+  po = (tile * fr.th + ly) * fr.tw + lx;
   return true;
 }
 
 // Pixel of this lane in a one-pixel-per-lane launch, or false if the lane has none.
 __device__ __forceinline__ bool pixel_setup(const DevFrame& fr, const wgt_tile* __restrict__ tiles,
-                                            uint32_t& tile, uint32_t& lx, uint32_t& ly, Pixel& px) {
-  return slot_setup(fr, tiles, blockIdx.x, threadIdx.x, tile, lx, ly, px);
+                                            uint32_t& po, Pixel& px) {
+  return slot_setup(fr, tiles, blockIdx.x, threadIdx.x, po, px);
 }
 
-// setup_camera_ray + pixel_sample_square (path_tracer.wgsl:232-262) for sample px.k
+// setup_camera_ray + pixel_sample_square (path_tracer.wgsl:232-262) for sample (px.si, px.sj)
 __device__ __forceinline__ void camera_ray(const DevFrame& fr, Pixel& px, f3& ro, f3& rd) {
   const f3 origin = f3{fr.ox, fr.oy, fr.oz};
   const f3 du = f3{fr.dux, fr.duy, fr.duz};
@@ -533,7 +537,6 @@ __device__ __forceinline__ void camera_ray(const DevFrame& fr, Pixel& px, f3& ro
 // col += max(path.col, 0) / f32(spp) (path_tracer.wgsl:393) and advance to the next sample
 __device__ __forceinline__ void end_sample(const DevFrame& fr, Pixel& px, f3 pc) {
   px.col = px.col + f3{max0(pc.x) / fr.fspp, max0(pc.y) / fr.fspp, max0(pc.z) / fr.fspp};
-  ++px.k;
   if (++px.si == fr.sqrt_spp) { px.si = 0; ++px.sj; }
 }
 
@@ -546,19 +549,16 @@ __device__ __forceinline__ void skip_nan_path(const DevScene& sc, const DevFrame
     c.q += (uint32_t)(kRayDepth - depth);
     c.nan += (uint32_t)(kRayDepth - depth);
   }
-  if (px.k == 0 && depth == 0) px.hit0 = last_prim(sc);
+  if (px_first(px) && depth == 0) px.hit0 = last_prim(sc);
   // col += max(NaN, 0) / spp == col + 0
-  ++px.k;
   if (++px.si == fr.sqrt_spp) { px.si = 0; ++px.sj; }
 }
 
-__device__ __forceinline__ void write_pixel(const DevFrame& fr, uint32_t tile, uint32_t lx,
-                                            uint32_t ly, const Pixel& px, uchar4* out8, float4* out32,
+__device__ __forceinline__ void write_pixel(uint32_t po, const Pixel& px, uchar4* out8, float4* out32,
                                             uint32_t* outhit) {
-  const size_t o = ((size_t)tile * fr.th + ly) * fr.tw + lx;
-  if (out32) out32[o] = make_float4(px.col.x, px.col.y, px.col.z, 1.0f);
-  if (out8) out8[o] = make_uchar4(unorm8(px.col.x), unorm8(px.col.y), unorm8(px.col.z), 255);
-  if (outhit) outhit[o] = px.hit0;
+  if (out32) out32[po] = make_float4(px.col.x, px.col.y, px.col.z, 1.0f);
+  if (out8) out8[po] = make_uchar4(unorm8(px.col.x), unorm8(px.col.y), unorm8(px.col.z), 255);
+  if (outhit) outhit[po] = px.hit0;
 }
 
 __device__ __forceinline__ void flush_counters(unsigned long long* __restrict__ counters,

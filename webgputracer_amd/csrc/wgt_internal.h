@@ -37,7 +37,6 @@ struct DevScene {
   uint32_t n_nodes;
   uint32_t last_sphere_emissive;
   float light_area;  // length(cross(lights[0].right, lights[0].up)) (path_tracer.wgsl:205)
-  uint32_t max_iters; // traversal safety bound on pops (4 x nodes + 8)
   uint32_t stack;     // traversal stack entries per lane (>= 1)
 };
 // Dynamic LDS bytes of a traversal kernel launch.

@@ -38,9 +38,9 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
          float4* __restrict__ out32, uint32_t* __restrict__ outhit,
          unsigned long long* __restrict__ counters) {
   extern __shared__ int s_stack[];  // sc.stack entries per lane (stack_lds_bytes)
-  uint32_t tile, lx, ly;
+  uint32_t po;
   Pixel px;
-  if (!pixel_setup(fr, tiles, tile, lx, ly, px)) return;
+  if (!pixel_setup(fr, tiles, po, px)) return;
   int* lds = s_stack + threadIdx.x;
   const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
   const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
@@ -49,7 +49,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
   TravStats st{0u, 0u, 0u, 0u};
   Counters c{0u, 0u, 0u, 0u, 0u, 1u};  // one pixel per lane
 
-  while (px.k < nsamp) {
+  while (!px_done(fr, px)) {
     if (STATS) simt_count(c.lw, c.ll);
     if (depth == 0) {
       camera_ray(fr, px, ro, rd);
@@ -67,7 +67,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
       ++c.q;
       if (nanray) ++c.nan; else ++c.tr;
     }
-    if (px.k == 0 && depth == 0) px.hit0 = h.prim;
+    if (px_first(px) && depth == 0) px.hit0 = h.prim;
     const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
     ++depth;
     if (end || depth == kRayDepth) {
@@ -75,7 +75,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
       depth = 0;
     }
   }
-  write_pixel(fr, tile, lx, ly, px, out8, out32, outhit);
+  write_pixel(po, px, out8, out32, outhit);
   if (STATS) flush_counters(counters, c, st, nsamp);
 }
 
@@ -115,7 +115,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
   const uint32_t n_slots = fr.n_slots;
   Pixel px{};
-  uint32_t tile = 0, lx = 0, ly = 0;
+  uint32_t po = 0;  // output offset of the lane's pixel
   f3 ro{}, rd{}, pc{};
   int depth = 0;
   TravStats st{0u, 0u, 0u, 0u};
@@ -126,6 +126,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   bool have = false;       // lane holds a pixel
   bool exhausted = false;  // the queue is empty for this lane
   bool trav = false, pending = false, fin = false;
+  bool nanray = false;  // the pending hit is a NaN ray's (emissive last sphere), resolved at finalise
   uint64_t cyc_svc = 0, cyc_trav = 0;
   uint64_t cr_refill = 0, cr_fin = 0, cr_shade = 0, cr_cam = 0, cr_quads = 0, cr_root = 0;
   uint32_t pblock = 0, work = 0;  // COST: the pixel's block and its work so far
@@ -140,7 +141,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           atomicAdd(fr.cost + pblock, work);
           work = 0;
         } else {
-          write_pixel(fr, tile, lx, ly, px, out8, out32, outhit);
+          write_pixel(po, px, out8, out32, outhit);
         }
         if (STATS) ++c.px;
         fin = false;
@@ -163,7 +164,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
               const uint32_t sb = COST ? (slot >> 4) : (slot >> 6);
               const uint32_t sl = COST ? (((slot & 3u) << 1) | (((slot >> 2) & 3u) << 4)) : (slot & 63u);
               const uint32_t b = fr.perm ? fr.perm[sb] : sb;
-              if (slot_setup(fr, tiles, b, sl, tile, lx, ly, px)) {
+              if (slot_setup(fr, tiles, b, sl, po, px)) {
                 have = true;
                 depth = 0;
                 pblock = b;
@@ -183,9 +184,15 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
         if (pending) {
           // finalise: rebuild the quad hit, merge triangles, scan spheres, shade
           Hit h;
-          WGT_REGION(cr_fin, quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h));
-          if (STATS) { ++c.q; ++c.tr; }
-          if (px.k == 0 && depth == 0) px.hit0 = h.prim;
+          if (nanray) {
+            nan_hit(sc, ro, rd, h);
+            if (STATS) { ++c.q; ++c.nan; }
+            nanray = false;
+          } else {
+            WGT_REGION(cr_fin, quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h));
+            if (STATS) { ++c.q; ++c.tr; }
+          }
+          if (px_first(px) && depth == 0) px.hit0 = h.prim;
           const uint64_t ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
           const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
           ++depth;
@@ -198,7 +205,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
         }
         // start the next ray of this pixel
         for (;;) {
-          if (px.k >= nsamp) {
+          if (px_done(fr, px)) {
             have = false;
             fin = true;
             break;
@@ -213,17 +220,11 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
               depth = 0;
               continue;
             }
-            Hit h;  // emissive last sphere: resolve the NaN ray here (no traversal)
-            nan_hit(sc, ro, rd, h);
-            if (STATS) { ++c.q; ++c.nan; }
-            if (px.k == 0 && depth == 0) px.hit0 = h.prim;
-            const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
-            ++depth;
-            if (end || depth == kRayDepth) {
-              end_sample(fr, px, pc);
-              depth = 0;
-            }
-            continue;
+            // emissive last sphere: the NaN ray's hit (the last sphere, no traversal)
+            // is resolved and shaded at the next finalise, the one shading site
+            nanray = true;
+            pending = true;
+            break;
           }
           Hit h;
           WGT_REGION(cr_quads, quad_scan(sc, ro, rd, h, q_t); q_prim = h.prim;

@@ -197,6 +197,10 @@ hipEvent_t pool_event(wgt_ctx* ctx, size_t i) {
 int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, uchar4* out8, float4* out32,
                  uint32_t* outhit, unsigned long long* counters, hipStream_t s, FrameTiming* timing) {
   const bool wavefront = ctx->sc.n_tris > 0 && fr.kernel == 0;
+  const uint64_t n64 = (uint64_t)fr.tw * fr.th * fr.n_tiles;
+  if (n64 == 0) return WGT_OK;
+  // 32-bit pixel offsets in the kernels (slot_setup, wf slots)
+  if (n64 > 0x7fffffffull) return fail(ctx, WGT_E_INVALID, "too many pixels in one launch");
   if (!wavefront) {
     hipEvent_t e0 = timing ? pool_event(ctx, 0) : nullptr, e1 = timing ? pool_event(ctx, 1) : nullptr;
     if (timing && (!e0 || !e1)) return fail(ctx, WGT_E_HIP, "hipEventCreate failed");
@@ -221,9 +225,6 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
     }
     return WGT_OK;
   }
-  const uint64_t n64 = (uint64_t)fr.tw * fr.th * fr.n_tiles;
-  if (n64 == 0) return WGT_OK;
-  if (n64 > 0x7fffffffull) return fail(ctx, WGT_E_INVALID, "too many pixels in one launch");
   const uint32_t n = (uint32_t)n64;
   int rc;
   if ((rc = ensure(ctx, ctx->wf, wf_state_bytes(n)))) return rc;
@@ -435,7 +436,6 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const f3 lr = f3{lights[0].right[0], lights[0].right[1], lights[0].right[2]};
   const f3 lu = f3{lights[0].up[0], lights[0].up[1], lights[0].up[2]};
   sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
-  sc.max_iters = 4u * bvh.n_nodes + 8u;
   // + 1: the speculative traversal parks a second leaf on the stack (wgt_device.h)
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
   WGT_HIP(ctx, ps_resident_waves(sc, ctx->device, ctx->ps_resident));

@@ -112,9 +112,11 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
   uint32_t tseed;
   slot_pixel(fr, tiles, s, px.x, px.y, tseed);
   px.seed = st.seed[s];
-  px.k = st.k[s];
-  px.si = px.k % fr.sqrt_spp;
-  px.sj = px.k / fr.sqrt_spp;
+  {
+    const uint32_t k = st.k[s];
+    px.si = k % fr.sqrt_spp;
+    px.sj = k / fr.sqrt_spp;
+  }
   px.col = ld3(st.col, n, s);
   px.hit0 = kNoHit;
   f3 pc = ld3(st.pc, n, s);
@@ -124,7 +126,7 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
   TravStats ts{0u, 0u, 0u, 0u};
 
   auto shade_and_advance = [&](const Hit& h) {
-    if (px.k == 0 && depth == 0 && outhit) outhit[s] = h.prim;
+    if (px_first(px) && depth == 0 && outhit) outhit[s] = h.prim;
     const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
     ++depth;
     if (end || depth == kRayDepth) {
@@ -139,7 +141,6 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
     Trav t;
     t.bi = st.res_i[s];
     t.bt = st.res_t[s];
-    t.found = t.bi != kNoHit;
     finish_hit(sc, ro, rd, t, h);
     if (STATS) { ++c.q; ++c.tr; }
     shade_and_advance(h);
@@ -148,7 +149,7 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
   uint32_t started = 0;
   for (;;) {
     if (STATS) simt_count(c.lw, c.ll);
-    if (px.k >= nsamp) {
+    if (px_done(fr, px)) {
       if (out32) out32[s] = make_float4(px.col.x, px.col.y, px.col.z, 1.0f);
       if (out8) out8[s] = make_uchar4(unorm8(px.col.x), unorm8(px.col.y), unorm8(px.col.z), 255);
       phase = PH_DONE;
@@ -165,7 +166,7 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
     }
     if (has_nan(ro) || has_nan(rd)) {
       if (!sc.last_sphere_emissive) {
-        if (px.k == 0 && depth == 0 && outhit) outhit[s] = last_prim(sc);
+        if (px_first(px) && depth == 0 && outhit) outhit[s] = last_prim(sc);
         skip_nan_path<STATS>(sc, fr, px, depth, c);
         depth = 0;
         continue;
@@ -188,14 +189,14 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
       break;
     }
     Trav none;
-    none.found = false;
+    none.bi = kNoHit;
     finish_hit(sc, ro, rd, none, h);
     if (STATS) { ++c.q; ++c.tr; }
     shade_and_advance(h);
   }
   st.dp[s] = (uint32_t)depth | (phase << 8);
   st.seed[s] = px.seed;
-  st.k[s] = px.k;
+  st.k[s] = px.si + px.sj * fr.sqrt_spp;
   st3(st.col, n, s, px.col);
   if (phase != PH_DONE) {
     st3(st.pc, n, s, pc);
@@ -263,7 +264,7 @@ k_wf_trace(DevScene sc, DevFrame fr, WfState st, unsigned long long* __restrict_
     }
     if (!__any(active)) break;
     if (active && trav_step<STATS>(sc, o, d, t, lds, ts)) {
-      st.res_i[slot] = t.found ? t.bi : kNoHit;
+      st.res_i[slot] = t.bi;
       st.res_t[slot] = t.bt;
       active = false;
     }
