@@ -128,8 +128,8 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.W = W;
   fr.H = H;
   fr.kernel = env_u32("WGT_KERNEL", 2);
-  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 16);  // swept on the persistent BVH4 kernel
-  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 14);
+  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 10);  // swept on the persistent BVH4 kernel
+  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 8);
   fr.tri_ratio = env_u32("WGT_TRI_RATIO", 100);
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
