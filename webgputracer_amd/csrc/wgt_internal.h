@@ -59,6 +59,10 @@ struct DevFrame {
   // once <= ps_to_service lanes still traverse.
   uint32_t kernel;  // scenes with triangles: 0 = wavefront, 1 = simple, 2 = phase-split (default)
   uint32_t ps_to_trav, ps_to_service;
+  // a wave with fewer live pixels leaves the traversal phase at <= live *
+  // ps_svc_frac / 64 traversing lanes (if lower): a sparse wave (the end of a
+  // launch) would otherwise pay a service pass for every finished ray (0 = off)
+  uint32_t ps_svc_frac;
   // speculative traversal: a triangle step runs when lanes with a pending leaf
   // number >= tri_ratio % of the lanes with a node to visit
   uint32_t tri_ratio;

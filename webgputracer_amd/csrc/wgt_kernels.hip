@@ -247,6 +247,12 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
     }
     if (__ballot(have || !exhausted) == 0ull) break;
     // --------------------------------------------------------- traversal phase
+    uint32_t to_service = fr.ps_to_service;
+    if (fr.ps_svc_frac) {
+      const uint32_t live = (uint32_t)__popcll(__ballot(have));
+      const uint32_t sparse = (live * fr.ps_svc_frac) >> 6;
+      to_service = sparse < to_service ? sparse : to_service;
+    }
     for (;;) {
       // one uniform mode per step: triangle steps once enough lanes hold a
       // pending leaf (weighted by the two steps' costs), else node steps
@@ -268,7 +274,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       }
       const uint32_t ntrav = (uint32_t)__popcll(__ballot(trav));
       if (ntrav == 0) break;
-      if (ntrav <= fr.ps_to_service && __any(!trav && (have || !exhausted))) break;
+      if (ntrav <= to_service && __any(!trav && (have || !exhausted))) break;
     }
     if (STATS) cyc_trav += __builtin_amdgcn_s_memtime() - t_phase;
   }

@@ -130,6 +130,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.kernel = env_u32("WGT_KERNEL", 2);
   fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 10);  // swept on the persistent BVH4 kernel
   fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 8);
+  fr.ps_svc_frac = env_u32("WGT_PS_SVC_FRAC", 16);  // sweep: profiles/sweeps/r01_ps_svc_frac.jsonl
   fr.tri_ratio = env_u32("WGT_TRI_RATIO", 100);
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
