@@ -62,7 +62,9 @@ __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict_
   const f3 w = xyz(wd);
   const float a = dot(w, cross(hit_vec, xyz(q[2])));
   const float b = dot(w, cross(xyz(q[1]), hit_vec));
-  if ((a < 0.0f) || (1.0f < a) || (b < 0.0f) || (1.0f < b)) return;
+  // (a < 0) || (1 < a) || (b < 0) || (1 < b), NaN included: IEEE minNum/maxNum
+  // return the non-NaN operand, and with both NaN every compare is false
+  if ((__builtin_fminf(a, b) < 0.0f) || (1.0f < __builtin_fmaxf(a, b))) return;
   quad_accept(o, d, q, id, t, ray_dist, h);
   qt = t;
 }
@@ -476,14 +478,19 @@ __device__ __forceinline__ uint8_t unorm8(float x) {
 struct Pixel {
   uint32_t x, y;
   uint32_t seed;
-  uint32_t si, sj;  // the sample's (s_i, s_j); sample index = si + sj * sqrt_spp
+  uint32_t sij;  // the sample's s_i | s_j << 16 (sqrt_spp < 2^16); index = s_i + s_j * sqrt_spp
   f3 col;
-  uint32_t hit0;
 };
 // all sqrt_spp^2 samples done (sj reaches sqrt_spp; at once when spp = 0)
-__device__ __forceinline__ bool px_done(const DevFrame& fr, const Pixel& px) { return px.sj >= fr.sqrt_spp; }
+__device__ __forceinline__ uint32_t px_si(const Pixel& px) { return px.sij & 0xffffu; }
+__device__ __forceinline__ uint32_t px_sj(const Pixel& px) { return px.sij >> 16; }
+__device__ __forceinline__ bool px_done(const DevFrame& fr, const Pixel& px) { return px_sj(px) >= fr.sqrt_spp; }
+// next (s_i, s_j) in the reference's loop order (path_tracer.wgsl:381-382)
+__device__ __forceinline__ void px_next(const DevFrame& fr, Pixel& px) {
+  px.sij = px_si(px) + 1u == fr.sqrt_spp ? (px.sij & 0xffff0000u) + 0x10000u : px.sij + 1u;
+}
 // sample 0 (the one whose first hit is the pixel's hit ID)
-__device__ __forceinline__ bool px_first(const Pixel& px) { return (px.si | px.sj) == 0u; }
+__device__ __forceinline__ bool px_first(const Pixel& px) { return px.sij == 0u; }
 
 struct Counters {
   uint32_t q, tr, nan, lw, ll;
@@ -508,9 +515,8 @@ __device__ __forceinline__ bool slot_setup(const DevFrame& fr, const wgt_tile* _
   px.y = td.y0 + ly;
   if (px.x >= fr.W || px.y >= fr.H) return false;  // path_tracer.wgsl:377
   px.seed = px.x + px.y * fr.W + td.seed * fr.W * fr.H;  // path_tracer.wgsl:378
-  px.si = px.sj = 0;
+  px.sij = 0u;
   px.col = f3{0.0f, 0.0f, 0.0f};
-  px.hit0 = kNoHit;
   po = (tile * fr.th + ly) * fr.tw + lx;
   return true;
 }
@@ -521,14 +527,14 @@ __device__ __forceinline__ bool pixel_setup(const DevFrame& fr, const wgt_tile* 
   return slot_setup(fr, tiles, blockIdx.x, threadIdx.x, po, px);
 }
 
-// setup_camera_ray + pixel_sample_square (path_tracer.wgsl:232-262) for sample (px.si, px.sj)
+// setup_camera_ray + pixel_sample_square (path_tracer.wgsl:232-262) for the sample (s_i, s_j) of px.sij
 __device__ __forceinline__ void camera_ray(const DevFrame& fr, Pixel& px, f3& ro, f3& rd) {
   const f3 origin = f3{fr.ox, fr.oy, fr.oz};
   const f3 du = f3{fr.dux, fr.duy, fr.duz};
   const f3 dv = f3{fr.dvx, fr.dvy, fr.dvz};
   const f3 pixel_center = (f3{fr.pox, fr.poy, fr.poz} + (float)px.x * du) + (float)px.y * dv;
-  const float sx = -0.5f + fr.recip_sqrt_spp * ((float)px.si + rand_next(px.seed));
-  const float sy = -0.5f + fr.recip_sqrt_spp * ((float)px.sj + rand_next(px.seed));
+  const float sx = -0.5f + fr.recip_sqrt_spp * ((float)px_si(px) + rand_next(px.seed));
+  const float sy = -0.5f + fr.recip_sqrt_spp * ((float)px_sj(px) + rand_next(px.seed));
   const f3 pixel_sample = pixel_center + (sx * du + sy * dv);
   ro = origin;
   rd = pixel_sample - origin;
@@ -537,7 +543,13 @@ __device__ __forceinline__ void camera_ray(const DevFrame& fr, Pixel& px, f3& ro
 // col += max(path.col, 0) / f32(spp) (path_tracer.wgsl:393) and advance to the next sample
 __device__ __forceinline__ void end_sample(const DevFrame& fr, Pixel& px, f3 pc) {
   px.col = px.col + f3{max0(pc.x) / fr.fspp, max0(pc.y) / fr.fspp, max0(pc.z) / fr.fspp};
-  if (++px.si == fr.sqrt_spp) { px.si = 0; ++px.sj; }
+  px_next(fr, px);
+}
+
+// The pixel's hit ID (path_tracer.wgsl:384-386): the primitive of sample 0's camera ray.
+__device__ __forceinline__ void first_hit(const Pixel& px, int depth, uint32_t prim, uint32_t po,
+                                          uint32_t* __restrict__ outhit) {
+  if (outhit && depth == 0 && px_first(px)) outhit[po] = prim;
 }
 
 // NaN-absorbed for the rest of the path: 3 rand() per remaining bounce, colour NaN.
@@ -549,16 +561,17 @@ __device__ __forceinline__ void skip_nan_path(const DevScene& sc, const DevFrame
     c.q += (uint32_t)(kRayDepth - depth);
     c.nan += (uint32_t)(kRayDepth - depth);
   }
-  if (px_first(px) && depth == 0) px.hit0 = last_prim(sc);
   // col += max(NaN, 0) / spp == col + 0
-  if (++px.si == fr.sqrt_spp) { px.si = 0; ++px.sj; }
+  px_next(fr, px);
 }
 
-__device__ __forceinline__ void write_pixel(uint32_t po, const Pixel& px, uchar4* out8, float4* out32,
-                                            uint32_t* outhit) {
+__device__ __forceinline__ void write_pixel(const DevFrame& fr, uint32_t po, const Pixel& px, uchar4* out8,
+                                            float4* out32, uint32_t* outhit) {
   if (out32) out32[po] = make_float4(px.col.x, px.col.y, px.col.z, 1.0f);
   if (out8) out8[po] = make_uchar4(unorm8(px.col.x), unorm8(px.col.y), unorm8(px.col.z), 255);
-  if (outhit) outhit[po] = px.hit0;
+  // the hit ID is written when sample 0's first hit is known (first_hit); a
+  // pixel without samples has none
+  if (outhit && fr.sqrt_spp == 0u) outhit[po] = kNoHit;
 }
 
 __device__ __forceinline__ void flush_counters(unsigned long long* __restrict__ counters,

@@ -57,6 +57,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
     }
     const bool nanray = has_nan(ro) || has_nan(rd);
     if (nanray && !sc.last_sphere_emissive) {
+      first_hit(px, depth, last_prim(sc), po, outhit);
       skip_nan_path<STATS>(sc, fr, px, depth, c);
       depth = 0;
       continue;
@@ -67,7 +68,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
       ++c.q;
       if (nanray) ++c.nan; else ++c.tr;
     }
-    if (px_first(px) && depth == 0) px.hit0 = h.prim;
+    first_hit(px, depth, h.prim, po, outhit);
     const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
     ++depth;
     if (end || depth == kRayDepth) {
@@ -75,7 +76,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
       depth = 0;
     }
   }
-  write_pixel(po, px, out8, out32, outhit);
+  write_pixel(fr, po, px, out8, out32, outhit);
   if (STATS) flush_counters(counters, c, st, nsamp);
 }
 
@@ -141,7 +142,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           atomicAdd(fr.cost + pblock, work);
           work = 0;
         } else {
-          write_pixel(po, px, out8, out32, outhit);
+          write_pixel(fr, po, px, out8, out32, outhit);
         }
         if (STATS) ++c.px;
         fin = false;
@@ -192,7 +193,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             WGT_REGION(cr_fin, quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h));
             if (STATS) { ++c.q; ++c.tr; }
           }
-          if (px_first(px) && depth == 0) px.hit0 = h.prim;
+          first_hit(px, depth, h.prim, po, outhit);
           const uint64_t ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
           const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
           ++depth;
@@ -216,6 +217,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           }
           if (has_nan(ro) || has_nan(rd)) {
             if (!sc.last_sphere_emissive) {
+              first_hit(px, depth, last_prim(sc), po, outhit);
               skip_nan_path<STATS>(sc, fr, px, depth, c);
               depth = 0;
               continue;

@@ -114,11 +114,9 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
   px.seed = st.seed[s];
   {
     const uint32_t k = st.k[s];
-    px.si = k % fr.sqrt_spp;
-    px.sj = k / fr.sqrt_spp;
+    px.sij = (k % fr.sqrt_spp) | ((k / fr.sqrt_spp) << 16);
   }
   px.col = ld3(st.col, n, s);
-  px.hit0 = kNoHit;
   f3 pc = ld3(st.pc, n, s);
   f3 ro = ld3(st.ro, n, s);
   f3 rd = ld3(st.rd, n, s);
@@ -196,7 +194,7 @@ k_wf_shade(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, WfState
   }
   st.dp[s] = (uint32_t)depth | (phase << 8);
   st.seed[s] = px.seed;
-  st.k[s] = px.si + px.sj * fr.sqrt_spp;
+  st.k[s] = px_si(px) + px_sj(px) * fr.sqrt_spp;
   st3(st.col, n, s, px.col);
   if (phase != PH_DONE) {
     st3(st.pc, n, s, pc);
