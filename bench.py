@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on fewer GPUs")
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="weak: one frame per GPU per step (default); strong: one frame split over the GPUs")
     p.add_argument("--check", action="store_true",
                    help="rank 0 compares the assembled frames with single-launch renders (bit-exact)")
     return p.parse_args()
@@ -132,9 +134,10 @@ def main():
     ctx.upload_scene(*scene)
     info = ctx.scene_info()
 
-    frames = [(j, j) for j in range(world)]  # this step's frames: (frame id, seed)
+    # this step's frames (frame id, seed): one per GPU (weak scaling) or one in all (strong)
+    frames = [(j, j) for j in range(world)] if args.scaling == "weak" else [(0, 0)]
     tiles = wdist.shard_tiles(W, H, T, frames, rank, world)
-    n_max = wdist.max_tiles_per_rank(W, H, T, world, world)
+    n_max = wdist.max_tiles_per_rank(W, H, T, len(frames), world)
     dev = torch.device("cuda", local)
     d_tiles = torch.from_numpy(tiles.view(np.uint8).copy()).to(dev)
     out = torch.zeros((n_max, T, T, 4), dtype=torch.uint8, device=dev)
@@ -233,14 +236,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(max_t / max(args.steps, 1) * 1e3, 3),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": f"synthetic: procedural {args.scene} stand-in ({n_tris} tris) in the reference Cornell box"
                     if args.scene != "cornell" else "synthetic: reference Cornell box",
             "config": {"workload": f"{args.scene}-{W}x{H}-{spp}spp", "width": W, "height": H, "spp": spp,
                        "triangles": n_tris, "bvh_nodes": info["bvh_nodes"], "tile": T,
-                       "frames_per_step": world,
+                       "frames_per_step": len(frames),
                        "parallelism": f"tiles{world}+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}-gather"},
             "samples_per_s": round(samples / max_t, 1),
             "reference_queries_per_s": round(queries / max_t, 1),

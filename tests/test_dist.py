@@ -59,7 +59,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, result_path):
+def _worker(rank, world, port, result_path, strong=False):
     import torch
     import torch.distributed as dist
 
@@ -69,9 +69,10 @@ def _worker(rank, world, port, result_path):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     W, H, T = 70, 45, 16
-    frames = [(j, j) for j in range(world)]
+    # weak scaling: one frame per rank; strong: one frame split over the ranks (bench.py --scaling)
+    frames = [(0, 0)] if strong else [(j, j) for j in range(world)]
     tiles = wd.shard_tiles(W, H, T, frames, rank, world)
-    n_max = wd.max_tiles_per_rank(W, H, T, world, world)
+    n_max = wd.max_tiles_per_rank(W, H, T, len(frames), world)
     local = np.zeros((n_max, T, T, 4), np.uint8)
     local[:len(tiles)] = render_tiles(tiles, T)
     bufs = wd.gather_tiles(torch.from_numpy(local), rank, world, dist)
@@ -87,11 +88,13 @@ def _worker(rank, world, port, result_path):
     dist.destroy_process_group()
 
 
-def test_gloo_world2_gather_assembles_frames(tmp_path):
+@pytest.mark.parametrize("strong", [False, True])
+def test_gloo_world2_gather_assembles_frames(tmp_path, strong):
     import torch.multiprocessing as mp
 
     result = tmp_path / "result.txt"
-    mp.start_processes(_worker, args=(2, _free_port(), str(result)), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_worker, args=(2, _free_port(), str(result), strong), nprocs=2, join=True,
+                       start_method="spawn")
     assert result.read_text() == "ok"
 
 
