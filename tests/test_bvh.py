@@ -15,7 +15,7 @@ import pytest
 import webgputracer_amd as w
 
 f32 = np.float32
-STACK_MAX = 36  # kStackMax (wgt_internal.h)
+STACK_MAX = 31  # kStackMax (wgt_internal.h)
 EMPTY = f32(3e38)  # kEmptySlotCoord (wgt_geom.h)
 
 

@@ -218,37 +218,60 @@ Child Child2(const std::vector<float>& n2, int id, int which) {
   return c;
 }
 
-// Greedy collapse: a BVH4 node starts from the two children of a BVH2 node and
-// repeatedly opens its largest-area internal child until it has 4 slots.  Returns
-// the BVH4 node index; `need` receives the worst-case stack entries of the
-// subtree: the traversal pushes at most (children - 1) per node on a root-to-node
-// path, so need = (children - 1) + max over internal children.
+// Budgeted greedy collapse: a BVH4 node starts from the two children of a BVH2
+// node and repeatedly opens its largest-area internal child until it has 4
+// slots.  Returns the BVH4 node index; `need` receives the worst-case stack
+// entries of the subtree: the traversal pushes at most (children - 1) per node
+// on a root-to-node path, so need = (children - 1) + max over internal children.
+// The stack is bounded by `budget`: a child is opened only while (children - 1)
+// + the least need any child can still reach (its BVH2 height: a 2-wide node
+// pushes one entry per level) fits, so only the deep, stack-heavy paths get
+// narrower nodes.  Any budget >= the BVH2 height is met.
 class Collapser {
  public:
-  // pairs = true: open only the BVH2 node's own two children (a BVH4 node = two
-  // BVH2 levels), so BVH4 depth <= ceil(BVH2 depth / 2): the bounded fallback.
-  Collapser(const std::vector<float>& n2, BvhOut& o, bool pairs) : n2_(n2), out_(o), pairs_(pairs) {}
+  Collapser(const std::vector<float>& n2, BvhOut& o) : n2_(n2), out_(o), h_(n2.size() / 16, 0u) {
+    for (size_t i = h_.size(); i-- > 0;) {  // children follow their parent (preorder)
+      uint32_t m = 0;
+      for (int w = 0; w < 2; ++w) {
+        const Child c = Child2(n2_, (int)i, w);
+        if (c.ref >= 0) m = std::max(m, h_[c.ref]);
+      }
+      h_[i] = 1u + m;
+    }
+  }
+  uint32_t Height(int id2) const { return h_[id2]; }
 
-  int Collapse(int id2, uint32_t depth, uint32_t& need) {
+  int Collapse(int id2, uint32_t depth, uint32_t budget, uint32_t& need) {
     Child ch[kBvhWidth];
     int n = 2;
     ch[0] = Child2(n2_, id2, 0);
     ch[1] = Child2(n2_, id2, 1);
-    const int orig = n;
-    bool opened[2] = {false, false};  // pairs mode: each original child opens once
+    bool blocked[kBvhWidth] = {false, false, false, false};
     while (n < kBvhWidth) {
       int best = -1;
       double ba = -1.0;
-      for (int i = 0; i < (pairs_ ? orig : n); ++i)
-        if (ch[i].ref >= 0 && ch[i].b.area() > ba && !(pairs_ && opened[i])) {
+      for (int i = 0; i < n; ++i)
+        if (ch[i].ref >= 0 && !blocked[i] && ch[i].b.area() > ba) {
           ba = ch[i].b.area();
           best = i;
         }
       if (best < 0) break;
+      // the node after opening `best`: n children, the least subtree need of each
+      uint32_t m = 0;
+      for (int i = 0; i < n; ++i)
+        if (i != best && ch[i].ref >= 0) m = std::max(m, h_[ch[i].ref]);
       const int r = ch[best].ref;
+      for (int w = 0; w < 2; ++w) {
+        const Child c = Child2(n2_, r, w);
+        if (c.ref >= 0) m = std::max(m, h_[c.ref]);
+      }
+      if ((uint32_t)n + m > budget) {  // (n + 1 children) - 1 + m
+        blocked[best] = true;
+        continue;
+      }
       ch[best] = Child2(n2_, r, 0);
       ch[n++] = Child2(n2_, r, 1);
-      if (best < 2) opened[best] = true;
+      blocked[best] = false;
     }
     const uint32_t id = (uint32_t)(out_.nodes.size() / kNode4Floats);
     out_.nodes.resize(out_.nodes.size() + kNode4Floats);
@@ -257,9 +280,9 @@ class Collapser {
     uint32_t sub = 0;
     for (int i = 0; i < n; ++i) {
       if (ch[i].ref >= 0) {
-        uint32_t s = 0;
-        refs[i] = Collapse(ch[i].ref, depth + 1, s);
-        sub = std::max(sub, s);
+        uint32_t sn = 0;
+        refs[i] = Collapse(ch[i].ref, depth + 1, budget - (uint32_t)(n - 1), sn);
+        sub = std::max(sub, sn);
       } else {
         refs[i] = ch[i].ref;
       }
@@ -282,7 +305,7 @@ class Collapser {
  private:
   const std::vector<float>& n2_;
   BvhOut& out_;
-  bool pairs_;
+  std::vector<uint32_t> h_;  // BVH2 height (internal levels) of every BVH2 node
 };
 
 }  // namespace
@@ -335,14 +358,13 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
   const double ra = root_box.area();
   if (ra > 0) out.sah_cost /= ra;
   out.nodes.reserve(n2.size() * 2);
-  Collapser greedy(n2, out, false);
-  greedy.Collapse(0, 0, out.stack_need);
-  if (out.stack_need > stack_limit) {
-    out.nodes.clear();
-    out.max_depth = 0;
-    Collapser pairs(n2, out, true);
-    pairs.Collapse(0, 0, out.stack_need);
+  Collapser greedy(n2, out);
+  if (greedy.Height(0) > stack_limit) {
+    err = "BuildBvh: BVH2 height " + std::to_string(greedy.Height(0)) + " exceeds the stack limit " +
+          std::to_string(stack_limit);
+    return false;
   }
+  greedy.Collapse(0, 0, stack_limit, out.stack_need);
   if (out.stack_need > stack_limit) {
     err = "BuildBvh: traversal stack " + std::to_string(out.stack_need) + " exceeds " +
           std::to_string(stack_limit);

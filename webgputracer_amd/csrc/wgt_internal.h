@@ -23,9 +23,11 @@ constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
 // Per-lane traversal stack in LDS, stride kBlock (conflict-free), sized per scene
 // at launch (dynamic LDS) to the builder's exact worst case DevScene::stack, so it
 // cannot overflow and needs no spill path.  kMaxBvhDepth bounds the SAH BVH2 the
-// BVH4 is collapsed from; kStackMax bounds the stack (9 KB per wave).
+// BVH4 is collapsed from; kStackMax bounds the builder's stack need: + 1 parking
+// slot = 32 entries = 8 KB per wave, so LDS admits the 5 waves per SIMD the
+// registers allow (20 per CU) on every scene.
 constexpr int kMaxBvhDepth = 24;
-constexpr int kStackMax = 36;
+constexpr int kStackMax = 31;
 
 struct DevScene {
   const float4* __restrict__ quads;   // n_lights + n_quads records

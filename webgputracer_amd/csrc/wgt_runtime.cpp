@@ -100,6 +100,9 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 
 // setup_camera_ray's frame-invariant terms (path_tracer.wgsl:239-257), same fp32
 // operations as the WGSL per-invocation evaluation.
+// The builder's stack bound (WGT_STACK_LIMIT overrides kStackMax for sweeps).
+uint32_t stack_limit() { return std::min(env_u32("WGT_STACK_LIMIT", (uint32_t)kStackMax), (uint32_t)kStackMax); }
+
 DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   DevFrame fr{};
   const float theta = radians_w(cam.fovy);
@@ -354,7 +357,7 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   if (!tris || n_tris == 0 || !info) return fail(nullptr, WGT_E_INVALID, "null triangles or info");
   BvhOut bvh;
   std::string err;
-  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, (uint32_t)kStackMax, bvh, err))
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), bvh, err))
     return fail(nullptr, WGT_E_INVALID, err);
   *info = wgt_scene_info{};
   info->n_tris = n_tris;
@@ -391,7 +394,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   BvhOut bvh;
   if (n_tris > 0) {
     std::string err;
-    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, (uint32_t)kStackMax, bvh, err)) return fail(ctx, WGT_E_INVALID, err);
+    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), bvh, err)) return fail(ctx, WGT_E_INVALID, err);
   }
   const uint32_t nlq = n_lights + n_quads;
   const size_t b_quads = align256((size_t)nlq * 96);
