@@ -123,3 +123,22 @@ def test_bvh_full_size_meshes_stack_bound():
         info, _, _ = w.bvh_build(w.procedural_mesh(kind))
         assert 1 <= info["bvh_stack"] <= STACK_MAX
         assert info["bvh2_depth"] <= 24 and info["bvh_max_leaf"] <= 8
+
+
+@pytest.mark.parametrize("limit", [24, 20, 16])
+def test_bvh_stack_budget(monkeypatch, limit):
+    """The budgeted collapse meets any stack bound >= the BVH2 height by narrowing
+    only stack-heavy nodes (WGT_STACK_LIMIT lowers kStackMax for the build): the
+    walk's exact need equals the reported one and stays within the bound."""
+    monkeypatch.setenv("WGT_STACK_LIMIT", str(limit))
+    tris = random_soup(5000, 11)
+    info = check_tree(tris)
+    assert info["bvh_stack"] <= limit
+    assert info["bvh2_depth"] <= limit  # feasibility: the BVH2 height fits
+
+
+def test_bvh_stack_budget_below_height_fails(monkeypatch):
+    """A bound below the BVH2 height cannot be met: the build fails loudly."""
+    monkeypatch.setenv("WGT_STACK_LIMIT", "3")
+    with pytest.raises(RuntimeError, match="stack limit"):
+        w.bvh_build(random_soup(5000, 11))
