@@ -1,11 +1,12 @@
 """bench.py — BASELINE.json metric: Mrays/sec at 1080p/256spp (+ achieved GB/s vs HBM peak).
 
-Workload (BASELINE configs[2], the largest single-GPU config): Stanford-Bunny-sized
-procedural stand-in (69,696 triangles; the asset is absent and there is no network)
-inside the reference Cornell box + light, 1920x1080, 256 spp.  A "step" renders one
-1080p/256spp frame per GPU: the step's N frames are cut into 32x32 tiles dealt
-round-robin over the N ranks (one process per GPU), then the tiles are gathered to
-rank 0 (RCCL over xGMI) and assembled — weak scaling, per-GPU work fixed.
+Workload (BASELINE configs[3], C4 — the config the metric's "1/2/4/8 MI355X" is quoted
+on, and the one north_star's roofline target names): Sponza-sized procedural stand-in
+(268,944 triangles; the asset is absent and there is no network) inside the reference
+Cornell box + light, 1920x1080, 256 spp.  `--scene bunny` runs configs[2] (C3).  A
+"step" renders one 1080p/256spp frame per GPU: the step's N frames are cut into 32x32
+tiles dealt round-robin over the N ranks (one process per GPU), then the tiles are
+gathered to rank 0 (RCCL over xGMI) and assembled — weak scaling, per-GPU work fixed.
 
 value = closest-hit queries actually traced (non-NaN rays, counted on the device by
 an instrumented pass over the same tiles) summed over ranks x steps / max-over-ranks
@@ -15,7 +16,7 @@ torch.cuda.Event pairs time exactly its launches (roofline.achieved): the 1-spp 
 pre-pass + LPT ordering (~0.5 % of the call at 256 spp) and the main kernel
 k_render_ps (the rocprof kernel trace under profiles/ lists them separately).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--scene bunny|sponza|cornell]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scene sponza|bunny|cornell]
   torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -46,7 +47,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--scene", default="bunny", choices=["bunny", "sponza", "cornell"])
+    p.add_argument("--scene", default="sponza", choices=["sponza", "bunny", "cornell"])
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--spp", type=int, default=256)
@@ -221,8 +222,8 @@ def main():
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
-            if (tj.get("workload") == f"{args.scene}-{W}x{H}-{spp}spp" and tj.get("n_gpus", 1) == 1 and world == 1
-                    and tj.get("kernel") == DOMINANT_KERNEL):
+            tj = tj.get(f"{args.scene}-{W}x{H}-{spp}spp", {})  # one entry per workload
+            if tj.get("n_gpus", 1) == 1 and world == 1 and tj.get("kernel") == DOMINANT_KERNEL:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass

@@ -73,10 +73,18 @@ def main():
         out += ["", f"HBM bytes per launch of `{timed}` = (2 x FETCH_SIZE + WRITE_SIZE) x 1024 = {hbm / 1e9:.3f} GB "
                     f"(FETCH doubled per MI355X_MICROARCH.md §HBM); L2 hit rate "
                     f"{hit / max(hit + miss, 1):.4f}."]
-        json.dump({"workload": line["config"]["workload"], "n_gpus": 1, "kernel": timed,
-                   "hbm_bytes_per_launch": hbm, "fetch_size_kib": fetch, "write_size_kib": write,
-                   "source": f"profiles/{rnd}_{tag}_summary.md"},
-                  open(os.path.join(dst, "pmc_traffic.json"), "w"), indent=1)
+        # one entry per workload (bench.py reads the entry of its own workload)
+        tpath = os.path.join(dst, "pmc_traffic.json")
+        try:
+            table = json.load(open(tpath))
+        except (OSError, ValueError):
+            table = {}
+        if "workload" in table:  # the old single-entry format
+            table = {table["workload"]: table}
+        wl = line["config"]["workload"]
+        table[wl] = {"workload": wl, "n_gpus": 1, "kernel": timed, "hbm_bytes_per_launch": hbm,
+                     "fetch_size_kib": fetch, "write_size_kib": write, "source": f"profiles/{rnd}_{tag}_summary.md"}
+        json.dump(table, open(tpath, "w"), indent=1)
     sq = {c: per.get((timed, c)) for c in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")}
     if all(v for v in sq.values()):
         wc = sq["SQ_WAVE_CYCLES"]

@@ -24,10 +24,16 @@ constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
 // at launch (dynamic LDS) to the builder's exact worst case DevScene::stack, so it
 // cannot overflow and needs no spill path.  kMaxBvhDepth bounds the SAH BVH2 the
 // BVH4 is collapsed from; kStackMax bounds the builder's stack need: + 1 parking
-// slot = 32 entries = 8 KB per wave, so LDS admits the 5 waves per SIMD the
-// registers allow (20 per CU) on every scene.
+// slot, so that LDS (160 KB per CU) admits kPsWaves waves per SIMD (4 SIMDs per
+// CU) on every scene: 5 waves -> 32 entries = 8 KB per wave, 6 -> 26 entries.
+// kPsWaves is also the register budget of k_render_ps (amdgpu_waves_per_eu).
+#ifndef WGT_PS_WAVES
+#define WGT_PS_WAVES 5
+#endif
+constexpr int kPsWaves = WGT_PS_WAVES;
 constexpr int kMaxBvhDepth = 24;
-constexpr int kStackMax = 31;
+constexpr int kStackMax = (160 * 1024) / (kPsWaves * 4 * kBlock * 4) - 1;
+static_assert(kStackMax >= 16 && kStackMax <= 31, "stack bound out of the tested range");
 
 struct DevScene {
   const float4* __restrict__ quads;   // n_lights + n_quads records

@@ -104,7 +104,7 @@ constexpr uint32_t kCostService = 7;  // a service iteration ~ 7 traversal steps
   } while (0)
 
 template <bool STATS, bool COST>
-__global__ void __launch_bounds__(kBlock)
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPsWaves)))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
             unsigned long long* __restrict__ counters, uint32_t* __restrict__ queue) {
