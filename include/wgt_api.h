@@ -206,6 +206,11 @@ int wgt_trace_rays_async(wgt_ctx *ctx, const float *d_rays, uint32_t n, uint32_t
                          float *d_dist, void *stream);
 
 int wgt_sync(wgt_ctx *ctx);
+/* Diagnostics: the kernels' short correctly-rounded sqrt / division sequences
+ * (wgt_math.h sqrt_rn, div_rn) against the IEEE operations on n pseudo-random
+ * inputs per operation from the ranges the kernels feed them; counts[0..3] =
+ * sqrt tests, sqrt mismatches, div tests, div mismatches (synchronous). */
+int wgt_selftest_math(wgt_ctx *ctx, uint32_t n, uint32_t seed, uint64_t counts[4]);
 /* The context's HIP stream (hipStream_t) for callers that share it. */
 void *wgt_stream(wgt_ctx *ctx);
 

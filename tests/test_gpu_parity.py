@@ -332,3 +332,13 @@ def test_cli_batched_frames_equal_reference_loop(tmp_path):
         outs[b] = [np.asarray(Image.open(d / f"{f:03d}.png").convert("RGBA")) for f in range(3)]
     for f in range(3):
         assert np.array_equal(outs[1][f], outs[3][f]), f
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_selftest_math_sequences_are_ieee(ctx, seed):
+    """The kernels' short sqrt / division sequences (wgt_math.h sqrt_rn, div_rn)
+    equal IEEE sqrt and division bit for bit over 16M inputs each from the ranges
+    the kernels feed them (specials included for sqrt)."""
+    ns, bs, nd, bd = ctx.selftest_math(1 << 24, seed)
+    assert ns == nd == 1 << 24
+    assert bs == 0 and bd == 0, (bs, bd)

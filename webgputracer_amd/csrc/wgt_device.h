@@ -53,7 +53,7 @@ __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict_
   const float denom = dot(qn, d);
   if (fabs_w(denom) < kRayMin) return;
   const float4 wd = q[4];
-  const float t = (wd.w - dot(qn, o)) / denom;
+  const float t = div_rn(wd.w - dot(qn, o), denom);
   if (t < kRayMin || kRayMax < t) return;
   const f3 pos = o + t * d;
   const float ray_dist = distance(pos, o);
@@ -80,7 +80,7 @@ __device__ __forceinline__ void isect_sphere(f3 o, f3 d, const float4* __restric
   const float c = dot(oc, oc) - cr.w * cr.w;
   const float disc = half_b * half_b - a * c;
   if (disc < 0.0f) return;
-  const float sqrt_d = __builtin_sqrtf(disc);
+  const float sqrt_d = sqrt_rn(disc);
   float root = (-half_b - sqrt_d) / a;
   if (root < kRayMin || kRayMax < root) {
     root = (-half_b + sqrt_d) / a;
@@ -435,11 +435,11 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
     const f3 u = cross(w, v);
     const float r1 = rand_next(seed);
     const float r2 = rand_next(seed);
-    const float z = __builtin_sqrtf(1.0f - r2);
+    const float z = sqrt_rn(1.0f - r2);
     const float phi = 2.0f * kPI * r1;
     float sphi, cphi;
     sincos_w(phi, sphi, cphi);
-    const float sr2 = __builtin_sqrtf(r2);
+    const float sr2 = sqrt_rn(r2);
     const float lx2 = cphi * sr2;
     const float ly2 = sphi * sr2;
     sdir = (lx2 * u + ly2 * v) + z * w;
@@ -542,7 +542,10 @@ __device__ __forceinline__ void camera_ray(const DevFrame& fr, Pixel& px, f3& ro
 
 // col += max(path.col, 0) / f32(spp) (path_tracer.wgsl:393) and advance to the next sample
 __device__ __forceinline__ void end_sample(const DevFrame& fr, Pixel& px, f3 pc) {
-  px.col = px.col + f3{max0(pc.x) / fr.fspp, max0(pc.y) / fr.fspp, max0(pc.z) / fr.fspp};
+  // x / 2^k == x * 2^-k exactly (one rounding of the same real value), so a
+  // power-of-two spp multiplies
+  const f3 m{max0(pc.x), max0(pc.y), max0(pc.z)};
+  px.col = px.col + (fr.inv_fspp != 0.0f ? fr.inv_fspp * m : m / fr.fspp);
   px_next(fr, px);
 }
 

@@ -50,6 +50,9 @@ struct DevScene {
 // Dynamic LDS bytes of a traversal kernel launch.
 inline size_t stack_lds_bytes(const DevScene& sc) { return (size_t)sc.stack * kBlock * sizeof(int); }
 
+// 1 / spp when spp is a power of two (exact in fp32: end_sample multiplies), else 0
+inline float pow2_recip(uint32_t spp) { return (spp != 0u && (spp & (spp - 1u)) == 0u) ? 1.0f / (float)spp : 0.0f; }
+
 // Per-frame camera constants of setup_camera_ray (path_tracer.wgsl:239-262),
 // computed once on the host with the same fp32 operations (wgt_math.h).
 struct DevFrame {
@@ -59,6 +62,7 @@ struct DevFrame {
   float dvx, dvy, dvz; // pixel_delta_v
   float recip_sqrt_spp;
   float fspp;          // f32(camera.spp)
+  float inv_fspp;      // 1 / fspp when spp is a power of two (exact), else 0
   uint32_t sqrt_spp;
   uint32_t W, H;
   uint32_t tw, th, n_tiles;
@@ -150,6 +154,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
                          hipStream_t stream);
 // Waves of k_render_ps resident on the whole device for this scene's LDS stack.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves);
+hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d_counts, hipStream_t stream);
 hipError_t launch_trace(const DevScene& sc, const float* d_rays, uint32_t n, uint32_t* prim,
                         float* dist, hipStream_t stream);
 

@@ -336,6 +336,43 @@ k_lpt_order(const uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __rest
   for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) perm[atomicAdd(&s_cnt[lpt_bucket(cost[i])], 1u)] = i;
 }
 
+// wgt_selftest_math: sqrt_rn / div_rn against IEEE sqrt and division.  Inputs are
+// hashed from (seed, i): sqrt over x = 0, +inf, negatives and x >= 2^-96 of every
+// exponent; div over |d| in [2^-10, 2^20] and |n| in [2^-40, 2^40], both signs.
+__device__ __forceinline__ uint32_t st_hash(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
+  return x;
+}
+__device__ __forceinline__ float st_float(uint32_t h, int emin, int emax) {
+  const uint32_t e = (uint32_t)(emin + 127) + (h >> 9) % (uint32_t)(emax - emin + 1);
+  return __uint_as_float((h & 0x80000000u) | (e << 23) | (st_hash(h) & 0x7fffffu));
+}
+__global__ void __launch_bounds__(256) k_selftest_math(uint32_t n, uint32_t seed, unsigned long long* counts) {
+  uint32_t bad_s = 0, bad_d = 0;
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const uint32_t h = st_hash(seed * 0x9e3779b9u + i);
+    float x = fabsf(st_float(h, -96, 127));
+    const uint32_t k = i & 1023u;
+    if (k == 0) x = 0.0f;
+    if (k == 1) x = __builtin_inff();
+    if (k == 2) x = -x;
+    if (k == 3) x = __uint_as_float(0x7fc00000u);
+    const float a = sqrt_rn(x), b = __builtin_sqrtf(x);
+    if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) ++bad_s;
+    const uint32_t h2 = st_hash(h ^ 0x5bd1e995u);
+    const float nn = st_float(h2, -40, 40), dd = st_float(st_hash(h2), -10, 20);
+    const float q = div_rn(nn, dd), r = nn / dd;
+    if (__float_as_uint(q) != __float_as_uint(r)) ++bad_d;
+  }
+  atomicAdd(&counts[1], (unsigned long long)bad_s);
+  atomicAdd(&counts[3], (unsigned long long)bad_d);
+}
+
+hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d_counts, hipStream_t stream) {
+  k_selftest_math<<<1024, 256, 0, stream>>>(n, seed, d_counts);
+  return hipGetLastError();
+}
+
 size_t render_ws_bytes(const DevFrame& fr) {
   const uint64_t bx = (fr.tw + 7u) / 8u, by = (fr.th + 7u) / 8u;
   return 256 + 8 * bx * by * fr.n_tiles;
@@ -371,6 +408,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       fc.sqrt_spp = fr.pq_lpt < fr.sqrt_spp ? fr.pq_lpt : fr.sqrt_spp;
       fc.recip_sqrt_spp = 1.0f / (float)fc.sqrt_spp;
       fc.fspp = (float)(fc.sqrt_spp * fc.sqrt_spp);
+      fc.inv_fspp = pow2_recip(fc.sqrt_spp * fc.sqrt_spp);
       fc.cost = (uint32_t*)((char*)ws + 256);
       fc.n_slots = nb * 16u;  // a quarter of each block's pixels estimate its cost
       k_render_ps<false, true><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);

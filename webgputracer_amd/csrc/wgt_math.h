@@ -42,7 +42,45 @@ WGT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 WGT_HD f3 cross(f3 a, f3 b) {
   return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-WGT_HD float length(f3 a) { return __builtin_sqrtf(dot(a, a)); }
+// Correctly rounded sqrt (device: fewer instructions than the general lowering).
+// The compiler lowers llvm.sqrt.f32 as: hardware v_sqrt_f32 (<= 1 ulp), then the
+// neighbour whose residual x - s*s brackets x, with an input scaling for
+// 0 < x < 2^-96 and a class fix-up for +-0 / +inf around it.  sqrt_rn is that
+// sequence without the scaling and the fix-up, which are identities for x = +-0,
+// x >= 2^-96, +inf and x < 0 / NaN (-> NaN).  Every sqrt input of the kernels is
+// one of those: squared lengths of scene-scale vectors (0 or >= 1e-8), rand()
+// values and 1 - rand() (0 or >= 2^-33), sphere discriminants (0 or >= ulp of
+// scene-scale squares).  tests/test_gpu_parity.py checks it against IEEE sqrt
+// (wgt_selftest_math) and every image bit for bit against the oracle.
+WGT_HD float sqrt_rn(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const float s = __builtin_amdgcn_sqrtf(x);
+  const float dn = __uint_as_float(__float_as_uint(s) - 1u);
+  const float up = __uint_as_float(__float_as_uint(s) + 1u);
+  const float rdn = __builtin_fmaf(-dn, s, x), rup = __builtin_fmaf(-up, s, x);
+  const float r = rdn <= 0.0f ? dn : s;
+  return rup > 0.0f ? up : r;
+#else
+  return __builtin_sqrtf(x);
+#endif
+}
+// Correctly rounded n / d for |d| >= 2^-100 and |n| <= 2^100 with a normal or zero
+// quotient (the quad plane distance: |d| >= kRayMin, scene-scale n): the
+// compiler's IEEE sequence (reciprocal refined by one Newton step, two residual
+// corrections) without v_div_scale / v_div_fixup, which are identities there.  A
+// -0 quotient may come out +0 (irrelevant where it is used: t = +-0 < kRayMin).
+WGT_HD float div_rn(float n, float d) {
+#ifdef __HIP_DEVICE_COMPILE__
+  float r = __builtin_amdgcn_rcpf(d);
+  r = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+  float q = n * r;
+  q = __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+  return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+#else
+  return n / d;
+#endif
+}
+WGT_HD float length(f3 a) { return sqrt_rn(dot(a, a)); }
 // WGSL normalize(v) = v / length(v)   (zero vector -> NaN, as the reference relies on)
 WGT_HD f3 normalize(f3 a) { return a / length(a); }
 WGT_HD float distance(f3 a, f3 b) { return length(a - b); }

@@ -127,6 +127,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.dvx = dv.x; fr.dvy = dv.y; fr.dvz = dv.z;
   fr.recip_sqrt_spp = 1.0f / __builtin_sqrtf((float)cam.spp);
   fr.fspp = (float)cam.spp;
+  fr.inv_fspp = pow2_recip(cam.spp);
   fr.sqrt_spp = (uint32_t)__builtin_sqrtf((float)cam.spp);
   fr.W = W;
   fr.H = H;
@@ -634,6 +635,20 @@ int wgt_trace_rays_async(wgt_ctx* ctx, const float* d_rays, uint32_t n, uint32_t
   WGT_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   WGT_HIP(ctx, launch_trace(ctx->sc, d_rays, n, d_prim_id, d_dist, s));
+  return WGT_OK;
+}
+
+int wgt_selftest_math(wgt_ctx* ctx, uint32_t n, uint32_t seed, uint64_t counts[4]) {
+  if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
+  if (!counts) return fail(ctx, WGT_E_INVALID, "null counts");
+  WGT_HIP(ctx, hipSetDevice(ctx->device));
+  int rc;
+  if ((rc = ensure(ctx, ctx->prim, 32))) return rc;
+  WGT_HIP(ctx, hipMemsetAsync(ctx->prim.p, 0, 32, ctx->stream));
+  WGT_HIP(ctx, launch_selftest_math(n, seed, (unsigned long long*)ctx->prim.p, ctx->stream));
+  WGT_HIP(ctx, hipMemcpyAsync(counts, ctx->prim.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  counts[0] = counts[2] = n;
   return WGT_OK;
 }
 

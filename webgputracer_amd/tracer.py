@@ -224,6 +224,12 @@ class Context:
     def sync(self):
         self._check(self._L.wgt_sync(self.h))
 
+    def selftest_math(self, n: int, seed: int = 1):
+        """-> (sqrt tests, sqrt mismatches, div tests, div mismatches) of wgt_selftest_math."""
+        counts = np.zeros(4, np.uint64)
+        self._check(self._L.wgt_selftest_math(self.h, n, seed, counts.ctypes.data_as(ctypes.c_void_p)))
+        return tuple(int(c) for c in counts)
+
 
 def tile_grid(W: int, H: int, T: int, seed: int = 0, frame: int = 0):
     """All T x T tiles of a W x H frame, row-major (x0, y0, seed, frame)."""
