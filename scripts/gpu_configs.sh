@@ -1,14 +1,14 @@
 #!/bin/bash
-# Every BASELINE config on one GPU: C2 Cornell 1024^2/64, C3 bunny 1080p/256 (bench default),
-# C4 sponza 1080p/256 (1 GPU share), C5 bunny 1080p/64 frames (batch 1 vs 4).
+# Every BASELINE config on one GPU: C2 Cornell 1024^2/64, C3 bunny 1080p/256,
+# C4 sponza 1080p/256 (bench default, 1 GPU share), C5 bunny 1080p/64 frames (batch 1 vs 4).
 #   bash scripts/gpu_configs.sh TAG
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
 OUT=gpurun_out/${1:-cfg}; mkdir -p $OUT
-timeout -k 10 900 python -m pytest tests/ -m gpu -q -x > $OUT/pytest_gpu.log 2>&1 || { tail -20 $OUT/pytest_gpu.log; exit 1; }
+timeout -k 10 600 python -u -m pytest tests/ -m gpu -q -x --timeout 120 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || { tail -20 $OUT/pytest_gpu.log; exit 1; }
 tail -1 $OUT/pytest_gpu.log
 timeout -k 10 600 python bench.py --scene cornell --width 1024 --height 1024 --spp 64 --steps 3 --warmup 1 --no-cpu-baseline > $OUT/c2.log 2>&1 || { tail $OUT/c2.log; exit 1; }
-timeout -k 10 600 python bench.py --steps 3 --warmup 1 --no-cpu-baseline > $OUT/c3.log 2>&1 || { tail $OUT/c3.log; exit 1; }
+timeout -k 10 600 python bench.py --scene bunny --steps 3 --warmup 1 --no-cpu-baseline > $OUT/c3.log 2>&1 || { tail $OUT/c3.log; exit 1; }
 timeout -k 10 900 python bench.py --scene sponza --steps 2 --warmup 1 --no-cpu-baseline > $OUT/c4.log 2>&1 || { tail $OUT/c4.log; exit 1; }
 timeout -k 10 600 python -m webgputracer_amd.frames --frame 1 16 --spp 64 --batch 1 > $OUT/c5_b1.log 2>&1 || { tail $OUT/c5_b1.log; exit 1; }
 timeout -k 10 600 python -m webgputracer_amd.frames --frame 1 16 --spp 64 --batch 4 > $OUT/c5_b4.log 2>&1 || { tail $OUT/c5_b4.log; exit 1; }
