@@ -35,11 +35,22 @@ sys.path.insert(0, ROOT)
 METRIC = "Mrays/sec at 1080p/256spp + achieved HBM GB/s vs peak, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # algorithmic bytes per unit: a BVH4 node visit reads 7 x 16 B (6 SoA
-# box rows + child refs) of its 128-B line, a triangle test 3 x 16 B of its 64-B
-# record (the 4th, the padded box, only for a candidate closest hit), a traced ray
-# 32 B of per-triangle shading data
-NODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 48, 32
-DOMINANT_KERNEL = "wgt::k_render_ps<false, false>"
+# box rows + child refs) of its 128-B line, or with compact nodes 4 x 16 B of its
+# 64-B node + its 16-B ref record; a triangle test 3 x 16 B of its 64-B record (the
+# 4th, the padded box, only for a candidate closest hit), a traced ray 32 B of
+# per-triangle shading data
+NODE_BYTES, CNODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 48, 32
+
+
+def dominant_kernel(compact: bool) -> str:
+    """The timed k_render_ps instantiation <STATS, COST, compact nodes>."""
+    return f"wgt::k_render_ps<false, false, {'true' if compact else 'false'}>"
+
+
+def compact_nodes(info) -> bool:
+    """The node form k_render_ps reads (WGT_CNODE: 0 = 128-B, 1 = compact, 2 = auto)."""
+    mode = os.environ.get("WGT_CNODE", "2") or "2"
+    return mode == "1" or (mode == "2" and bool(info.get("bvh_compact", 0)))
 
 
 def parse():
@@ -215,15 +226,18 @@ def main():
 
     base = cpu_baseline(args, scene, rank, world)
     if rank == 0:
-        # dominant kernel = DOMINANT_KERNEL; algorithmic bytes of rank 0's launch
-        bytes_launch = (mine[4] * NODE_BYTES + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
+        # dominant kernel = k_render_ps; algorithmic bytes of rank 0's launch
+        compact = compact_nodes(info)
+        kernel = dominant_kernel(compact)
+        node_b = CNODE_BYTES if compact else NODE_BYTES
+        bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         traffic = None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             tj = tj.get(f"{args.scene}-{W}x{H}-{spp}spp", {})  # one entry per workload
-            if tj.get("n_gpus", 1) == 1 and world == 1 and tj.get("kernel") == DOMINANT_KERNEL:
+            if tj.get("n_gpus", 1) == 1 and world == 1 and tj.get("kernel") == kernel:
                 traffic = tj.get("hbm_bytes_per_launch")
         except (OSError, ValueError):
             pass
@@ -251,8 +265,9 @@ def main():
             "kernel_ms": round(kern_ms, 3),
             "simt_utilisation": {k: round(v, 4) for k, v in simt.items()},
             "per_launch": {"traced_rays": int(mine[1]), "node_visits": int(mine[4]), "tri_tests": int(mine[5]),
-                           "algorithmic_bytes": int(bytes_launch),
-                           "bytes_per_unit": {"node": NODE_BYTES, "tri": TRI_BYTES, "shade_per_ray": SHADE_BYTES}},
+                           "algorithmic_bytes": int(bytes_launch), "kernel": kernel,
+                           "bvh_nodes": "compact 64 B + 16 B refs" if compact else "128 B",
+                           "bytes_per_unit": {"node": node_b, "tri": TRI_BYTES, "shade_per_ray": SHADE_BYTES}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
             "cpu_baseline": base,

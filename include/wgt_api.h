@@ -131,6 +131,9 @@ typedef struct {
   uint32_t bvh_width;    /* children per node (4) */
   uint32_t bvh_stack;    /* worst-case traversal stack entries per ray (LDS) */
   uint32_t bvh2_nodes, bvh2_depth;
+  uint32_t bvh_compact;   /* 1: the tree exceeds one XCD's L2 as 128-B nodes, so the persistent
+                           * kernel reads its compact form (64-B nodes + 16-B refs) by default */
+  float bvh_compact_step; /* scene-wide decode step of the compact nodes (wgt_geom.h) */
 } wgt_scene_info;
 
 typedef struct wgt_ctx wgt_ctx;
@@ -158,6 +161,11 @@ int wgt_scene_info_get(const wgt_ctx *ctx, wgt_scene_info *info);
  * Call once with NULL outputs to size them. */
 int wgt_bvh_build(const wgt_triangle *tris, uint32_t n_tris, float *nodes_out, uint32_t nodes_cap,
                   float *tris_out, wgt_scene_info *info);
+/* Host only: the compact form of the same tree (wgt_geom.h): cnodes_out gets
+ * bvh_nodes x 16 words, crefs_out bvh_nodes x 4 child refs, step_out the decode
+ * step.  Both outputs are required; nodes_cap must be >= bvh_nodes. */
+int wgt_bvh_build_compact(const wgt_triangle *tris, uint32_t n_tris, uint32_t *cnodes_out,
+                          int32_t *crefs_out, uint32_t nodes_cap, float *step_out);
 
 /* ---- rendering (replaces the compute pass of Renderer::OnRender) --------- */
 /* Synchronous: render the rectangle [x0,x0+tw) x [y0,y0+th) of a W x H frame

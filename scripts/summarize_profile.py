@@ -63,8 +63,7 @@ def main():
             per[(k, c)] = v
             out.append(f"| `{k}` | {c} | {v:,.1f} |")
     sys.path.insert(0, ROOT)
-    from bench import DOMINANT_KERNEL
-    timed = DOMINANT_KERNEL
+    timed = line["per_launch"]["kernel"]
     fetch = per.get((timed, "FETCH_SIZE"))
     write = per.get((timed, "WRITE_SIZE"))
     if fetch is not None and write is not None:

@@ -142,3 +142,65 @@ def test_bvh_stack_budget_below_height_fails(monkeypatch):
     monkeypatch.setenv("WGT_STACK_LIMIT", "3")
     with pytest.raises(RuntimeError, match="stack limit"):
         w.bvh_build(random_soup(5000, 11))
+
+
+def check_compact(tris):
+    """The compact node form (wgt_geom.h) of the same tree: every live child box
+    decodes (fma(h, step, org), exact product + one rounding, as numpy f32 h*step + org)
+    to a box containing the 128-B child box, each code is the tightest such
+    binary16 value, empty slots are masked, refs are the 128-B node's refs."""
+    info, nodes, _ = w.bvh_build(tris)
+    cn, cr, step = w.bvh_build_compact(tris)
+    step = f32(step)
+    assert step > 0 and np.log2(step) == np.round(np.log2(step))  # a power of two
+    assert cn.shape == (info["bvh_nodes"], 16)
+    np.testing.assert_array_equal(cr, nodes[:, 6, :].view(np.int32))
+    org = cn[:, 0:3].view(np.float32)
+    meta = cn[:, 3]
+    live = ~((nodes[:, 0, :] == EMPTY) & (nodes[:, 1, :] == EMPTY))  # (n, 4)
+    for s in range(4):
+        np.testing.assert_array_equal(((meta >> (24 + s)) & 1) == 1, ~live[:, s])
+    assert ((meta & 0x00FFFFFF) == 0).all()
+
+    def codes(words):  # (n, 2) words -> (n, 4) half bit patterns, children 0..3
+        return np.stack([words[:, 0] & 0xFFFF, words[:, 0] >> 16, words[:, 1] & 0xFFFF, words[:, 1] >> 16], 1)
+
+    def dec(h, o):
+        return h.astype(np.uint16).view(np.float16).astype(f32) * step + o[:, None]
+
+    for a in range(3):
+        lo_h, hi_h = codes(cn[:, 4 + 4 * a:6 + 4 * a]), codes(cn[:, 6 + 4 * a:8 + 4 * a])
+        assert (lo_h <= 0x7BFF).all() and (hi_h <= 0x7BFF).all()  # finite, non-negative halves
+        blo, bhi = nodes[:, 2 * a, :], nodes[:, 2 * a + 1, :]
+        dlo, dhi = dec(lo_h, org[:, a]), dec(hi_h, org[:, a])
+        assert (dlo[live] <= blo[live]).all() and (dhi[live] >= bhi[live]).all()
+        # tightest: the next code outward would no longer contain the bound
+        up = live & (lo_h < 0x7BFF)
+        assert (dec(lo_h + 1, org[:, a])[up] > blo[up]).all()
+        down = live & (hi_h > 0)
+        assert (dec(hi_h - 1, org[:, a])[down] < bhi[down]).all()
+        # org = the union's lower bound
+        np.testing.assert_array_equal(org[:, a], np.where(live, blo, np.inf).min(1))
+    return info
+
+
+@pytest.mark.parametrize("n,seed", [(1, 0), (9, 3), (5000, 5)])
+def test_compact_nodes_random_soup(n, seed):
+    check_compact(random_soup(n, seed))
+
+
+def test_compact_nodes_wide_and_tiny_extents():
+    # a 1e6-wide scene (step > 1) with millimetre triangles (subnormal-range codes)
+    rng = np.random.default_rng(7)
+    v0 = rng.uniform(-5e5, 5e5, (2000, 3)).astype(f32)
+    v = np.stack([v0, v0 + rng.normal(0, 1e-3, (2000, 3)).astype(f32), v0 + rng.normal(0, 1e-3, (2000, 3)).astype(f32)], 1)
+    check_compact(w.make_triangles(v))
+
+
+def test_compact_nodes_full_size_meshes():
+    """Auto rule: the bunny stand-in's 128-B tree (2.3 MB) fits one XCD's 4 MB L2 and
+    keeps the 128-B nodes; sponza's (8.5 MB) does not, so the persistent kernel reads
+    the compact form."""
+    for kind, compact in (("bunny", 0), ("sponza", 1)):
+        tris = w.procedural_mesh(kind)
+        assert check_compact(tris)["bvh_compact"] == compact

@@ -225,17 +225,45 @@ def test_bunny_1080p_256spp_subsample(ctx, wgt, oracle, bunny):
         assert np.array_equal(g["hit"], r["hit"])
 
 
-def test_sponza_render_parity(ctx, wgt, oracle):
-    L, Q, S, T = wgt.mesh_scene("sponza")
+_SPONZA = {}
+
+
+@pytest.mark.parametrize("cnode", ["2", "0"])
+def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
+    """Sponza stand-in: by default (2) the persistent kernel reads the compact nodes
+    (the 128-B tree exceeds one XCD's L2), 0 forces the 128-B nodes."""
+    monkeypatch.setenv("WGT_CNODE", cnode)
+    if not _SPONZA:
+        L, Q, S, T = wgt.mesh_scene("sponza")
+        osc = oracle.OracleScene(L, Q, S, T)
+        _SPONZA["scene"] = (L, Q, S, T)
+        _SPONZA["r"] = osc.render(oracle.camera_param(16 / 9, 4, 5), 80, 45)
+    L, Q, S, T = _SPONZA["scene"]
     ctx.upload_scene(L, Q, S, T)
-    osc = oracle.OracleScene(L, Q, S, T)
     g = ctx.render_tile(wgt.camera_param(16 / 9, 4, 5), 80, 45, stats=True)
-    r = osc.render(oracle.camera_param(16 / 9, 4, 5), 80, 45)
+    r = _SPONZA["r"]
     assert_radiance(g["f32"], r["f32"])
     assert np.array_equal(g["hit"], r["hit"])
     check_counters(g["stats"], r["counters"], oracle)
     info = ctx.scene_info()
     assert info["n_tris"] == len(T) and info["bvh_max_depth"] <= 94
+    assert info["bvh_compact"] == 1
+
+
+def test_sponza_1080p_256spp_subsample_compact(ctx, wgt, oracle):
+    """BASELINE config 4 (the bench workload) at full size through the compact nodes:
+    GPU tiles of the 1920x1080/256spp frame vs the oracle on the same global pixels."""
+    if not _SPONZA:
+        pytest.skip("needs test_sponza_render_parity's scene")
+    L, Q, S, T = _SPONZA["scene"]
+    ctx.upload_scene(L, Q, S, T)
+    osc = oracle.OracleScene(L, Q, S, T)
+    cam_g, cam_o = wgt.camera_param(16 / 9, 256, 0), oracle.camera_param(16 / 9, 256, 0)
+    for (x0, y0) in [(960, 540), (300, 800)]:
+        g = ctx.render_tile(cam_g, 1920, 1080, x0, y0, 8, 2)
+        r = osc.render(cam_o, 1920, 1080, x0, y0, 8, 2)
+        assert_radiance(g["f32"], r["f32"])
+        assert np.array_equal(g["hit"], r["hit"])
 
 
 @pytest.mark.parametrize("kernel", ["0", "1", "2"])
@@ -259,11 +287,12 @@ _SCHED_REF = {}
 
 @pytest.mark.parametrize("env", [{"WGT_PQ_LPT": "0"}, {"WGT_PQ_LPT": "1"}, {"WGT_PQ_REFILL": "1"},
                                  {"WGT_PQ_REFILL": "64"}, {"WGT_PS_TO_TRAV": "1", "WGT_PS_TO_SERVICE": "63"},
-                                 {"WGT_PQ_LPT": "2"}, {"WGT_PS_SVC_FRAC": "0"}, {"WGT_PS_SVC_FRAC": "1"}])
+                                 {"WGT_PQ_LPT": "2"}, {"WGT_PS_SVC_FRAC": "0"}, {"WGT_PS_SVC_FRAC": "1"},
+                                 {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the
     cost pre-pass (1 or 4 spp) or block order; refill threshold; phase thresholds and
-    their sparse-wave scaling)
+    their sparse-wave scaling; the node form: compact nodes forced on the bunny)
     change which lane renders which pixel and when, never a bit of the result.  100x60
     leaves ragged 8x8 blocks at the frame edge.  The test runs after the kernel-family
     tests on the same context, the sequence that exposed a workspace-reuse bug (each

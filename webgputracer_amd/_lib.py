@@ -51,7 +51,8 @@ class WgtSceneInfo(ctypes.Structure):
                 ("n_tris", ctypes.c_uint32), ("bvh_nodes", ctypes.c_uint32), ("bvh_leaves", ctypes.c_uint32),
                 ("bvh_max_depth", ctypes.c_uint32), ("bvh_max_leaf", ctypes.c_uint32),
                 ("device_bytes", ctypes.c_uint64), ("sah_cost", ctypes.c_double), ("bvh_width", ctypes.c_uint32),
-                ("bvh_stack", ctypes.c_uint32), ("bvh2_nodes", ctypes.c_uint32), ("bvh2_depth", ctypes.c_uint32)]
+                ("bvh_stack", ctypes.c_uint32), ("bvh2_nodes", ctypes.c_uint32), ("bvh2_depth", ctypes.c_uint32),
+                ("bvh_compact", ctypes.c_uint32), ("bvh_compact_step", ctypes.c_float)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -63,7 +64,7 @@ EXPORTS = [
     "wgt_upload_scene", "wgt_scene_info_get", "wgt_render_tile", "wgt_render_tiles_async",
     "wgt_render_tiles_stats", "wgt_render_tiles_profile", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_selftest_math", "wgt_stream",
     "wgt_scene_cornell", "wgt_make_triangles", "wgt_load_obj", "wgt_procedural_mesh",
-    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build", "wgt_render_frames",
+    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build", "wgt_bvh_build_compact", "wgt_render_frames",
 ]
 
 _lib = None

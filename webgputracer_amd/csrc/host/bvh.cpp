@@ -308,6 +308,73 @@ class Collapser {
   std::vector<uint32_t> h_;  // BVH2 height (internal levels) of every BVH2 node
 };
 
+// Compact form of one node (wgt_geom.h): lo codes are the largest binary16
+// value (bit patterns of non-negative halves order like their values) whose
+// decoded plane is <= the exact bound, hi codes the smallest whose plane is >= it.
+float CDec(uint32_t h, float s, float org) { return qdec(half_bits_to_float(h), s, org); }
+void CompactNode(const float* n, float s, uint32_t* q) {
+  uint32_t meta = 0;
+  bool live[kBvhWidth];
+  for (int i = 0; i < kBvhWidth; ++i) live[i] = !(n[i] == kEmptySlotCoord && n[4 + i] == kEmptySlotCoord);
+  float org[3];
+  for (int a = 0; a < 3; ++a) {
+    float ulo = std::numeric_limits<float>::infinity();
+    for (int i = 0; i < kBvhWidth; ++i)
+      if (live[i]) ulo = std::min(ulo, n[(2 * a) * 4 + i]);
+    org[a] = ulo;
+    uint32_t lo_h[kBvhWidth], hi_h[kBvhWidth];
+    for (int i = 0; i < kBvhWidth; ++i) {
+      lo_h[i] = 0x7bffu;  // an empty slot: inverted box, masked anyway
+      hi_h[i] = 0u;
+      if (!live[i]) continue;
+      const float blo = n[(2 * a) * 4 + i], bhi = n[(2 * a + 1) * 4 + i];
+      uint32_t l = 0, r = 0x7bffu;  // largest h with CDec(h) <= blo (CDec(0) = ulo <= blo)
+      while (l < r) {
+        const uint32_t m = (l + r + 1) / 2;
+        if (CDec(m, s, ulo) <= blo) l = m; else r = m - 1;
+      }
+      lo_h[i] = l;
+      l = 0; r = 0x7bffu;  // smallest h with CDec(h) >= bhi (the step guarantees h = 65504 does)
+      while (l < r) {
+        const uint32_t m = (l + r) / 2;
+        if (CDec(m, s, ulo) >= bhi) r = m; else l = m + 1;
+      }
+      hi_h[i] = l;
+    }
+    q[4 + 4 * a + 0] = lo_h[0] | (lo_h[1] << 16);
+    q[4 + 4 * a + 1] = lo_h[2] | (lo_h[3] << 16);
+    q[4 + 4 * a + 2] = hi_h[0] | (hi_h[1] << 16);
+    q[4 + 4 * a + 3] = hi_h[2] | (hi_h[3] << 16);
+  }
+  for (int i = 0; i < kBvhWidth; ++i)
+    if (!live[i]) meta |= 1u << (24 + i);
+  std::memcpy(&q[0], org, 12);
+  q[3] = meta;
+}
+
+// The smallest power-of-two step with which code 65504 reaches every node's upper bounds.
+float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes) {
+  int e = -24;
+  for (;;) {
+    const float s = std::ldexp(1.0f, e);
+    bool ok = true;
+    for (uint32_t k = 0; k < n_nodes && ok; ++k) {
+      const float* n = &nodes[(size_t)k * kNode4Floats];
+      for (int a = 0; a < 3 && ok; ++a) {
+        float ulo = std::numeric_limits<float>::infinity(), uhi = -ulo;
+        for (int i = 0; i < kBvhWidth; ++i)
+          if (!(n[i] == kEmptySlotCoord && n[4 + i] == kEmptySlotCoord)) {
+            ulo = std::min(ulo, n[(2 * a) * 4 + i]);
+            uhi = std::max(uhi, n[(2 * a + 1) * 4 + i]);
+          }
+        ok = qdec(65504.0f, s, ulo) >= uhi;
+      }
+    }
+    if (ok) return s;
+    ++e;
+  }
+}
+
 }  // namespace
 
 bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
@@ -385,6 +452,13 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
         return false;
       }
     }
+  }
+  out.cstep = CompactStep(out.nodes, out.n_nodes);
+  out.cnodes.resize((size_t)out.n_nodes * kCNodeFloats);
+  out.crefs.resize((size_t)out.n_nodes * 4);
+  for (uint32_t i = 0; i < out.n_nodes; ++i) {
+    CompactNode(&out.nodes[(size_t)i * kNode4Floats], out.cstep, &out.cnodes[(size_t)i * kCNodeFloats]);
+    std::memcpy(&out.crefs[(size_t)i * 4], &out.nodes[(size_t)i * kNode4Floats + 24], 16);
   }
   out.tris.resize((size_t)n * kTriRecordFloats);
   for (uint32_t i = 0; i < n; ++i) {

@@ -13,6 +13,9 @@ namespace wgt {
 
 struct BvhOut {
   std::vector<float> nodes;   // kNode4Floats per BVH4 node (wgt_geom.h layout), root = 0
+  std::vector<uint32_t> cnodes;  // kCNodeFloats words per node: the compact form (wgt_geom.h)
+  std::vector<int32_t> crefs;    // 4 child refs per node (the compact form's ref records)
+  float cstep = 1.0f;            // scene-wide decode step of the compact nodes
   std::vector<float> tris;    // kTriRecordFloats per triangle, leaf order (wgt_geom.h)
   std::vector<float> tshade;  // 8 floats per original triangle
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;  // BVH4 nodes / depth

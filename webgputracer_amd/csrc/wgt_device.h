@@ -55,6 +55,10 @@ __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict_
   const float4 wd = q[4];
   const float t = div_rn(wd.w - dot(qn, o), denom);
   if (t < kRayMin || kRayMax < t) return;
+  // ray_dist is monotone non-decreasing in t >= 0 (each rounded step is), so t >=
+  // qt (the accepted quad's t) implies ray_dist >= h.dist: the `>=` rejection
+  // below, decided before the square root.  qt is +inf until a quad is accepted.
+  if (t >= qt) return;
   const f3 pos = o + t * d;
   const float ray_dist = distance(pos, o);
   if (ray_dist >= h.dist) return;
@@ -103,7 +107,7 @@ __device__ __forceinline__ void isect_sphere(f3 o, f3 d, const float4* __restric
 
 __device__ __forceinline__ void quad_scan(const DevScene& sc, f3 o, f3 d, Hit& h, float& qt) {
   hit_init(h);
-  qt = kRayMax;
+  qt = __builtin_inff();
   const uint32_t nlq = sc.n_lights + sc.n_quads;
   for (uint32_t k = 0; k < nlq; ++k) isect_quad(o, d, sc.quads + 6 * k, k, h, qt);
 }
@@ -186,6 +190,62 @@ __device__ __forceinline__ uint32_t child_key(const Trav& t, float lx, float hx,
                                   __builtin_fminf(__builtin_fmaxf(t0z, t1z), t.bt));
   return n <= f ? ((__float_as_uint(n) & ~3u) | slot) : kMissKey;
 }
+// Sort keys and refs of the 4 children of node `ref`, read from the 128-B nodes
+// (CN = false) or from the compact nodes (CN = true, wgt_geom.h).
+__device__ __forceinline__ float hcode(uint32_t w, uint32_t slot) {
+  return (float)__builtin_bit_cast(_Float16, (uint16_t)((slot & 1u) ? (w >> 16) : (w & 0xffffu)));
+}
+// Compact node: per axis the ray's entry plane is the lo code for inv >= 0 and the
+// hi code for inv < 0 (one select per two children), which equals the min / max
+// form of child_key because the slab formula is monotone in the plane.  The
+// decode fma(h, s, org) takes h from a half word (v_fma_mix_f32).
+__device__ __forceinline__ uint32_t cchild_key(const Trav& t, const uint32_t* nw, const uint32_t* fw, f3 org,
+                                               float s, uint32_t meta, uint32_t slot) {
+  const uint32_t k = slot >> 1;
+  const float tnx = __builtin_fmaf(qdec(hcode(nw[0 + k], slot), s, org.x), t.inv.x, t.ot.x);
+  const float tfx = __builtin_fmaf(qdec(hcode(fw[0 + k], slot), s, org.x), t.inv.x, t.ot.x);
+  const float tny = __builtin_fmaf(qdec(hcode(nw[2 + k], slot), s, org.y), t.inv.y, t.ot.y);
+  const float tfy = __builtin_fmaf(qdec(hcode(fw[2 + k], slot), s, org.y), t.inv.y, t.ot.y);
+  const float tnz = __builtin_fmaf(qdec(hcode(nw[4 + k], slot), s, org.z), t.inv.z, t.ot.z);
+  const float tfz = __builtin_fmaf(qdec(hcode(fw[4 + k], slot), s, org.z), t.inv.z, t.ot.z);
+  const float n = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, kRayMin));
+  const float f = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, t.bt));
+  const bool hit = n <= f && ((meta >> (24u + slot)) & 1u) == 0u;
+  return hit ? ((__float_as_uint(n) & ~3u) | slot) : kMissKey;
+}
+template <bool CN>
+__device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int ref, uint32_t& k0, uint32_t& k1,
+                                          uint32_t& k2, uint32_t& k3, int& r0, int& r1, int& r2, int& r3) {
+  if (CN) {
+    const float4* __restrict__ n = sc.cnodes + 4 * ref;
+    const float4 a = n[0];
+    const uint4 x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]),
+                z = __builtin_bit_cast(uint4, n[3]);
+    const int4 rf = sc.crefs[ref];
+    const uint32_t meta = __float_as_uint(a.w);
+    const f3 org = f3{a.x, a.y, a.z};
+    const bool sx = t.inv.x < 0.0f, sy = t.inv.y < 0.0f, sz = t.inv.z < 0.0f;
+    const uint32_t nw[6] = {sx ? x.z : x.x, sx ? x.w : x.y, sy ? y.z : y.x,
+                            sy ? y.w : y.y, sz ? z.z : z.x, sz ? z.w : z.y};
+    const uint32_t fw[6] = {sx ? x.x : x.z, sx ? x.y : x.w, sy ? y.x : y.z,
+                            sy ? y.y : y.w, sz ? z.x : z.z, sz ? z.y : z.w};
+    r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
+    k0 = cchild_key(t, nw, fw, org, sc.cstep, meta, 0u);
+    k1 = cchild_key(t, nw, fw, org, sc.cstep, meta, 1u);
+    k2 = cchild_key(t, nw, fw, org, sc.cstep, meta, 2u);
+    k3 = cchild_key(t, nw, fw, org, sc.cstep, meta, 3u);
+  } else {
+    const float4* __restrict__ n = sc.nodes + 8 * ref;
+    const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
+    const float4 rf = n[6];
+    r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z), r3 = __float_as_int(rf.w);
+    k0 = child_key(t, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, 0u);
+    k1 = child_key(t, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, 1u);
+    k2 = child_key(t, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, 2u);
+    k3 = child_key(t, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, 3u);
+  }
+}
+
 // Compare-exchange of (key, ref) pairs: the smaller key (and its ref) to a.
 __device__ __forceinline__ void cas(uint32_t& ka, int& ra, uint32_t& kb, int& rb) {
   const bool sw = kb < ka;
@@ -232,16 +292,10 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
     if (t.lf < t.le) return false;
     pop = true;
   } else {
-    const float4* __restrict__ n = sc.nodes + 8 * t.ref;
-    const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
-    const float4 rf = n[6];
     if (STATS) st.nodes++;
-    int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z),
-        r3 = __float_as_int(rf.w);
-    uint32_t k0 = child_key(t, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, 0u);
-    uint32_t k1 = child_key(t, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, 1u);
-    uint32_t k2 = child_key(t, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, 2u);
-    uint32_t k3 = child_key(t, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, 3u);
+    uint32_t k0, k1, k2, k3;
+    int r0, r1, r2, r3;
+    node_keys<false>(sc, t, t.ref, k0, k1, k2, k3, r0, r1, r2, r3);
     cas(k0, r0, k1, r1);
     cas(k2, r2, k3, r3);
     cas(k0, r0, k2, r2);
@@ -315,18 +369,12 @@ __device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int ca
 __device__ __forceinline__ bool trav_done(const Trav& t) { return t.ref == kNoRef && t.lf >= t.le && t.sp == 0; }
 
 // Visit t.ref: sort the hit children, push all but the nearest, place the nearest.
-template <bool STATS>
+template <bool STATS, bool CN>
 __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, int* __restrict__ lds, TravStats& st) {
-  const float4* __restrict__ n = sc.nodes + 8 * t.ref;
-  const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
-  const float4 rf = n[6];
   if (STATS) st.nodes++;
-  int r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z),
-      r3 = __float_as_int(rf.w);
-  uint32_t k0 = child_key(t, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, 0u);
-  uint32_t k1 = child_key(t, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, 1u);
-  uint32_t k2 = child_key(t, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, 2u);
-  uint32_t k3 = child_key(t, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, 3u);
+  uint32_t k0, k1, k2, k3;
+  int r0, r1, r2, r3;
+  node_keys<CN>(sc, t, t.ref, k0, k1, k2, k3, r0, r1, r2, r3);
   cas(k0, r0, k1, r1);
   cas(k2, r2, k3, r3);
   cas(k0, r0, k2, r2);

@@ -41,6 +41,9 @@ struct DevScene {
   const float4* __restrict__ nodes;
   const float4* __restrict__ tris;
   const float4* __restrict__ tshade;
+  const float4* __restrict__ cnodes;  // the same tree as compact nodes (wgt_geom.h)
+  const int4* __restrict__ crefs;     // their child refs
+  float cstep;                        // scene-wide decode step of the compact nodes
   uint32_t n_lights, n_quads, n_spheres, n_tris;
   uint32_t n_nodes;
   uint32_t last_sphere_emissive;
@@ -78,6 +81,9 @@ struct DevFrame {
   // speculative traversal: a triangle step runs when lanes with a pending leaf
   // number >= tri_ratio % of the lanes with a node to visit
   uint32_t tri_ratio;
+  // BVH node form of k_render_ps: 0 = 128-B nodes, 1 = compact nodes, 2 = compact
+  // when the 128-B tree exceeds kCompactNodeBytes (default)
+  uint32_t cnode;
   // wavefront: rays a slot may start per shade launch, slots per trace wave,
   // idle lanes that trigger a refill from the wave's ray list
   uint32_t wf_rays, wf_chunk, wf_refill;
@@ -152,6 +158,8 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
                          uchar4* out8, float4* out32, uint32_t* outhit,
                          unsigned long long* counters, uint32_t resident, void* ws, size_t ws_cap,
                          hipStream_t stream);
+// Whether k_render_ps reads the compact node form for this scene and frame (DevFrame::cnode).
+bool use_compact_nodes(const DevScene& sc, const DevFrame& fr);
 // Waves of k_render_ps resident on the whole device for this scene's LDS stack.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves);
 hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d_counts, hipStream_t stream);

@@ -103,7 +103,7 @@ constexpr uint32_t kCostService = 7;  // a service iteration ~ 7 traversal steps
     if (STATS) acc += __builtin_amdgcn_s_memtime() - r0_;     \
   } while (0)
 
-template <bool STATS, bool COST>
+template <bool STATS, bool COST, bool CN>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPsWaves)))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
@@ -234,7 +234,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           if (COST) work += kCostService;
           // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
-          WGT_REGION(cr_root, node_step<STATS>(sc, t, lds, st));
+          WGT_REGION(cr_root, node_step<STATS, CN>(sc, t, lds, st));
           if (trav_done(t)) pending = true;
           else trav = true;
           break;
@@ -268,7 +268,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       if (tri_mode) {
         if (can_tri) tri_step<STATS>(sc, ro, rd, t, lds, st);
       } else {
-        if (can_node) node_step<STATS>(sc, t, lds, st);
+        if (can_node) node_step<STATS, CN>(sc, t, lds, st);
       }
       if (trav && trav_done(t)) {
         trav = false;
@@ -373,6 +373,13 @@ hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d
   return hipGetLastError();
 }
 
+// k_render_ps reads the compact nodes when asked to, or by default when the 128-B
+// tree would not fit one XCD's 4 MB L2 (sponza stand-in: 8.5 MB -> 4.3 + 1.1 MB);
+// a tree that fits keeps the 128-B nodes, whose step needs fewer VALU.
+bool use_compact_nodes(const DevScene& sc, const DevFrame& fr) {
+  return fr.cnode == 1 || (fr.cnode == 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes);
+}
+
 size_t render_ws_bytes(const DevFrame& fr) {
   const uint64_t bx = (fr.tw + 7u) / 8u, by = (fr.th + 7u) / 8u;
   return 256 + 8 * bx * by * fr.n_tiles;
@@ -397,6 +404,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
     // workspace (the context's, used in stream order): [0] pre-pass queue,
     // [1] queue | cost[nb] | perm[nb]
     const bool lpt = fr.pq_lpt && fr.sqrt_spp > fr.pq_lpt;
+    const bool cn = use_compact_nodes(sc, fr);
     uint32_t* q = (uint32_t*)ws;
     DevFrame f = fr;
     f.n_slots = nb * 64u;
@@ -411,14 +419,20 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       fc.inv_fspp = pow2_recip(fc.sqrt_spp * fc.sqrt_spp);
       fc.cost = (uint32_t*)((char*)ws + 256);
       fc.n_slots = nb * 16u;  // a quarter of each block's pixels estimate its cost
-      k_render_ps<false, true><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
+      if (cn) k_render_ps<false, true, true><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
+      else k_render_ps<false, true, false><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
       k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb);
       f.perm = fc.cost + nb;
       e = hipGetLastError();
     }
     if (e == hipSuccess) {
-      if (counters) k_render_ps<true, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, counters, q + 1);
-      else k_render_ps<false, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
+      if (counters) {
+        if (cn) k_render_ps<true, false, true><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, counters, q + 1);
+        else k_render_ps<true, false, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, counters, q + 1);
+      } else {
+        if (cn) k_render_ps<false, false, true><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
+        else k_render_ps<false, false, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
+      }
       e = hipGetLastError();
     }
     return e;
@@ -435,18 +449,21 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
 }
 
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
-  int per_cu_plain = 0, per_cu_stats = 0, cus = 0;
-  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu_plain, reinterpret_cast<const void*>(&k_render_ps<false, false>), kBlock, stack_lds_bytes(sc));
-  if (e != hipSuccess) return e;
-  e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-      &per_cu_stats, reinterpret_cast<const void*>(&k_render_ps<true, false>), kBlock, stack_lds_bytes(sc));
-  if (e != hipSuccess) return e;
-  e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
-  if (e != hipSuccess) return e;
-  // the larger of the two variants' capacities: waves beyond a variant's capacity
+  const void* variants[4] = {reinterpret_cast<const void*>(&k_render_ps<false, false, false>),
+                             reinterpret_cast<const void*>(&k_render_ps<true, false, false>),
+                             reinterpret_cast<const void*>(&k_render_ps<false, false, true>),
+                             reinterpret_cast<const void*>(&k_render_ps<true, false, true>)};
+  // the largest of the variants' capacities: waves beyond a variant's capacity
   // start as others retire and find the queue drained or nearly so
-  const int per_cu = per_cu_plain > per_cu_stats ? per_cu_plain : per_cu_stats;
+  int per_cu = 0, cus = 0;
+  for (const void* k : variants) {
+    int n = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, stack_lds_bytes(sc));
+    if (e != hipSuccess) return e;
+    per_cu = n > per_cu ? n : per_cu;
+  }
+  const hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
+  if (e != hipSuccess) return e;
   waves = (uint32_t)((per_cu > 0 ? per_cu : 1) * (cus > 0 ? cus : 1));
   return hipSuccess;
 }

@@ -136,6 +136,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 8);
   fr.ps_svc_frac = env_u32("WGT_PS_SVC_FRAC", 16);  // sweep: profiles/sweeps/r01_ps_svc_frac.jsonl
   fr.tri_ratio = env_u32("WGT_TRI_RATIO", 100);
+  fr.cnode = env_u32("WGT_CNODE", 2);  // compact nodes once the 128-B tree outgrows an XCD's L2
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
   fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
@@ -377,6 +378,23 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
     std::memcpy(nodes_out, bvh.nodes.data(), bvh.nodes.size() * 4);
   }
   if (tris_out) std::memcpy(tris_out, bvh.tris.data(), bvh.tris.size() * 4);
+  info->bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
+  info->bvh_compact_step = bvh.cstep;
+  return WGT_OK;
+}
+
+int wgt_bvh_build_compact(const wgt_triangle* tris, uint32_t n_tris, uint32_t* cnodes_out, int32_t* crefs_out,
+                          uint32_t nodes_cap, float* step_out) {
+  if (!tris || n_tris == 0 || !cnodes_out || !crefs_out || !step_out)
+    return fail(nullptr, WGT_E_INVALID, "null triangles or outputs");
+  BvhOut bvh;
+  std::string err;
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), bvh, err))
+    return fail(nullptr, WGT_E_INVALID, err);
+  if (nodes_cap < bvh.n_nodes) return fail(nullptr, WGT_E_INVALID, "node capacity too small");
+  std::memcpy(cnodes_out, bvh.cnodes.data(), bvh.cnodes.size() * 4);
+  std::memcpy(crefs_out, bvh.crefs.data(), bvh.crefs.size() * 4);
+  *step_out = bvh.cstep;
   return WGT_OK;
 }
 
@@ -400,10 +418,14 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const uint32_t nlq = n_lights + n_quads;
   const size_t b_quads = align256((size_t)nlq * 96);
   const size_t b_sph = align256((size_t)n_spheres * 32);
+  // both node forms stay resident (the compact one is 40% of the 128-B one); the
+  // launch picks one per frame (DevFrame::cnode)
   const size_t b_nodes = align256(bvh.nodes.size() * 4);
+  const size_t b_cnodes = align256(bvh.cnodes.size() * 4);
+  const size_t b_crefs = align256(bvh.crefs.size() * 4);
   const size_t b_tris = align256(bvh.tris.size() * 4);
   const size_t b_shade = align256(bvh.tshade.size() * 4);
-  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade;
+  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_crefs;
 
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->scene_mem) {
@@ -422,6 +444,9 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     std::memcpy(host.data() + b_quads + b_sph + b_nodes, bvh.tris.data(), bvh.tris.size() * 4);
     std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris, bvh.tshade.data(),
                 bvh.tshade.size() * 4);
+    char* c = host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade;
+    std::memcpy(c, bvh.cnodes.data(), bvh.cnodes.size() * 4);
+    std::memcpy(c + b_cnodes, bvh.crefs.data(), bvh.crefs.size() * 4);
   }
   WGT_HIP(ctx, hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
 
@@ -432,6 +457,9 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.nodes = (const float4*)(base + b_quads + b_sph);
   sc.tris = (const float4*)(base + b_quads + b_sph + b_nodes);
   sc.tshade = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris);
+  sc.cnodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade);
+  sc.crefs = (const int4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes);
+  sc.cstep = bvh.cstep;
   sc.n_lights = n_lights;
   sc.n_quads = n_quads;
   sc.n_spheres = n_spheres;
@@ -461,6 +489,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   in.bvh_stack = n_tris ? std::max(bvh.stack_need, 1u) : 0u;
   in.bvh2_nodes = bvh.n_nodes2;
   in.bvh2_depth = bvh.depth2;
+  in.bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
+  in.bvh_compact_step = bvh.cstep;
   ctx->has_scene = true;
   return WGT_OK;
 }

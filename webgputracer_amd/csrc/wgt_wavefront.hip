@@ -85,12 +85,9 @@ k_wf_init(DevFrame fr, const wgt_tile* __restrict__ tiles, WfState st, uchar4* _
 __device__ __forceinline__ bool root_needs_trav(const DevScene& sc, f3 o, f3 d, bool quad_hit, float qt) {
   Trav t;
   trav_init(o, d, quad_hit, qt, t);
-  const float4* __restrict__ n = sc.nodes;
-  const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
-  const uint32_t k0 = child_key(t, lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, 0u);
-  const uint32_t k1 = child_key(t, lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, 1u);
-  const uint32_t k2 = child_key(t, lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, 2u);
-  const uint32_t k3 = child_key(t, lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, 3u);
+  uint32_t k0, k1, k2, k3;
+  int r0, r1, r2, r3;
+  node_keys<false>(sc, t, 0, k0, k1, k2, k3, r0, r1, r2, r3);
   return (k0 & k1 & k2 & k3) != kMissKey;  // a hit key has bit 31 clear
 }
 

@@ -96,6 +96,20 @@ def bvh_build(tris):
     return info.as_dict(), nodes, recs
 
 
+def bvh_build_compact(tris):
+    """Host-only compact form of the same tree (wgt_bvh_build_compact):
+    (cnodes (n, 16) u32, crefs (n, 4) i32, step)."""
+    tris = np.ascontiguousarray(tris, TRI_DTYPE)
+    L = lib()
+    info = WgtSceneInfo()
+    check(L.wgt_bvh_build(ptr(tris), len(tris), None, 0, None, ctypes.byref(info)))
+    cn = np.zeros((info.bvh_nodes, 16), np.uint32)
+    cr = np.zeros((info.bvh_nodes, 4), np.int32)
+    step = ctypes.c_float(0.0)
+    check(L.wgt_bvh_build_compact(ptr(tris), len(tris), ptr(cn), ptr(cr), info.bvh_nodes, ctypes.byref(step)))
+    return cn, cr, step.value
+
+
 def camera_param(aspect: float, spp: int, seed: int, fovy: float = 40.0):
     """Camera::Update (camera.cpp:64-70) with an explicit seed instead of RandSeed()."""
     cam = np.zeros(1, CAMERA_DTYPE)
