@@ -44,7 +44,13 @@ struct Prim {
   uint32_t idx;
 };
 
-constexpr int kBins = 32;
+constexpr int kMaxBins = 256;
+// SAH bins per axis (WGT_SAH_BINS, <= kMaxBins; tuning sweeps)
+int SahBins() {
+  const char* v = std::getenv("WGT_SAH_BINS");
+  const int n = v && *v ? std::atoi(v) : 32;
+  return std::max(2, std::min(n, kMaxBins));
+}
 
 // Depth of a median-split subtree over `count` primitives (leaves <= kLeafMax).
 uint32_t MedianDepth(uint32_t count) {
@@ -102,21 +108,21 @@ class Builder {
       for (int axis = 0; axis < 3; ++axis) {
         const float ext = cb.hi[axis] - cb.lo[axis];
         if (!(ext > 0.0f)) continue;
-        Box bb[kBins];
-        uint32_t bn[kBins] = {};
-        for (auto& b : bb) b.reset();
-        const double scale = kBins / (double)ext;
+        Box bb[kMaxBins];
+        uint32_t bn[kMaxBins] = {};
+        for (int k = 0; k < bins_; ++k) bb[k].reset();
+        const double scale = bins_ / (double)ext;
         for (uint32_t i = begin; i < end; ++i) {
-          int k = std::min(kBins - 1, (int)((prims_[i].c[axis] - cb.lo[axis]) * scale));
+          int k = std::min(bins_ - 1, (int)((prims_[i].c[axis] - cb.lo[axis]) * scale));
           bb[k].grow(prims_[i].b);
           bn[k]++;
         }
-        double rarea[kBins];
-        uint32_t rcount[kBins];
+        double rarea[kMaxBins];
+        uint32_t rcount[kMaxBins];
         Box acc;
         acc.reset();
         uint32_t n = 0;
-        for (int k = kBins - 1; k > 0; --k) {
+        for (int k = bins_ - 1; k > 0; --k) {
           acc.grow(bb[k]);
           n += bn[k];
           rarea[k] = acc.area();
@@ -124,7 +130,7 @@ class Builder {
         }
         acc.reset();
         n = 0;
-        for (int k = 0; k < kBins - 1; ++k) {
+        for (int k = 0; k < bins_ - 1; ++k) {
           acc.grow(bb[k]);
           n += bn[k];
           if (n == 0 || rcount[k + 1] == 0) continue;
@@ -140,9 +146,9 @@ class Builder {
       const double leaf_cost = kCostTri * count;
       if (best_axis >= 0 && !(count <= sah_leaf_ && leaf_cost <= split_cost)) {
         const float ext = cb.hi[best_axis] - cb.lo[best_axis];
-        const double scale = kBins / (double)ext;
+        const double scale = bins_ / (double)ext;
         auto it = std::partition(prims_.begin() + begin, prims_.begin() + end, [&](const Prim& p) {
-          int k = std::min(kBins - 1, (int)((p.c[best_axis] - cb.lo[best_axis]) * scale));
+          int k = std::min(bins_ - 1, (int)((p.c[best_axis] - cb.lo[best_axis]) * scale));
           return k <= best_bin;
         });
         mid = (uint32_t)(it - prims_.begin());
@@ -200,6 +206,7 @@ class Builder {
   uint32_t limit_;
   double cost_trav_ = SahTravCost();
   uint32_t sah_leaf_ = SahLeafMax();
+  int bins_ = SahBins();
 };
 
 

@@ -217,11 +217,11 @@ template <bool CN>
 __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int ref, uint32_t& k0, uint32_t& k1,
                                           uint32_t& k2, uint32_t& k3, int& r0, int& r1, int& r2, int& r3) {
   if (CN) {
-    const float4* __restrict__ n = sc.cnodes + 4 * ref;
+    const float4* __restrict__ n = sc.cnodes + kCRecordFloat4s * ref;
+    const int4 rf = __builtin_bit_cast(int4, n[4]);
     const float4 a = n[0];
     const uint4 x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]),
                 z = __builtin_bit_cast(uint4, n[3]);
-    const int4 rf = sc.crefs[ref];
     const uint32_t meta = __float_as_uint(a.w);
     const f3 org = f3{a.x, a.y, a.z};
     const bool sx = t.inv.x < 0.0f, sy = t.inv.y < 0.0f, sz = t.inv.z < 0.0f;

@@ -103,22 +103,26 @@ constexpr int kBvhWidth = 4;
 constexpr float kEmptySlotCoord = 3e38f;
 constexpr int kNode4Floats = 32;
 constexpr int kLeafMax = 8;
-// Compact BVH4 node, 64 B (4 x float4, half a cache line) + a 16-B ref record in
-// a separate array: the same tree as the 128-B nodes with every child plane
-// stored as a binary16 code h >= 0, decoded as qdec(h, s, org_a) = fma(h, s, org_a)
-// (one rounding of an exact product, monotone in h) with one scene-wide power-of-
-// two step s:
+// Compact BVH4 node: an 80-B record (5 x float4) = a 64-B node + its 16-B child
+// refs; the same tree as the 128-B nodes with every child plane stored as a
+// binary16 code h >= 0, decoded as qdec(h, s, org_a) = fma(h, s, org_a) (one
+// rounding of an exact product, monotone in h) with one scene-wide power-of-two
+// step s:
 //   C[0] = (org.x, org.y, org.z, meta)   org = lower bounds of the children's
 //          union; meta bits 24..27: slot i empty (masked: never entered)
 //   C[1] = lo.x of children (0|1, 2|3 as half pairs), hi.x (0|1, 2|3)
 //   C[2] = lo.y, hi.y                     C[3] = lo.z, hi.z
-//   R    = child refs (int4), as in N[6]
+//   C[4] = child refs (int bits), as N[6]
 // The builder picks each lo code as the largest whose plane decodes <= the exact
 // bound and each hi code as the smallest whose plane decodes >= it, so a decoded
 // box contains its 128-B box and, through it, every triangle box below: the
 // nesting argument of DESIGN.md §3.4 holds unchanged.  Kernels read this form when
-// the 128-B tree exceeds kCompactNodeBytes (one XCD's L2).
-constexpr int kCNodeFloats = 16;
+// the 128-B tree exceeds kCompactNodeBytes (one XCD's L2).  The
+// record is not line-aligned (80 of 128 B): half the records span two lines, yet
+// measured faster than refs in a separate array (two lines per visit) or 128-B
+// records (the full footprint).
+constexpr int kCNodeFloats = 16;     // the node part, as exported by wgt_bvh_build_compact
+constexpr int kCRecordFloat4s = 5;  // node + refs, the device record
 constexpr size_t kCompactNodeBytes = (size_t)4 << 20;
 WGT_HD float qdec(float code, float step, float org) { return __builtin_fmaf(code, step, org); }
 WGT_HD float half_bits_to_float(uint32_t b) {

@@ -41,8 +41,7 @@ struct DevScene {
   const float4* __restrict__ nodes;
   const float4* __restrict__ tris;
   const float4* __restrict__ tshade;
-  const float4* __restrict__ cnodes;  // the same tree as compact nodes (wgt_geom.h)
-  const int4* __restrict__ crefs;     // their child refs
+  const float4* __restrict__ cnodes;  // the same tree as 80-B compact records (wgt_geom.h)
   float cstep;                        // scene-wide decode step of the compact nodes
   uint32_t n_lights, n_quads, n_spheres, n_tris;
   uint32_t n_nodes;

@@ -418,14 +418,19 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const uint32_t nlq = n_lights + n_quads;
   const size_t b_quads = align256((size_t)nlq * 96);
   const size_t b_sph = align256((size_t)n_spheres * 32);
-  // both node forms stay resident (the compact one is 40% of the 128-B one); the
+  // both node forms stay resident (the compact one is 63% of the 128-B one); the
   // launch picks one per frame (DevFrame::cnode)
   const size_t b_nodes = align256(bvh.nodes.size() * 4);
-  const size_t b_cnodes = align256(bvh.cnodes.size() * 4);
-  const size_t b_crefs = align256(bvh.crefs.size() * 4);
+  // compact records: the 64-B node followed by its 16-B refs (wgt_geom.h)
+  std::vector<uint32_t> crec((size_t)bvh.n_nodes * kCRecordFloat4s * 4);
+  for (size_t i = 0; i < bvh.n_nodes; ++i) {
+    std::memcpy(&crec[i * kCRecordFloat4s * 4], &bvh.cnodes[i * kCNodeFloats], kCNodeFloats * 4);
+    std::memcpy(&crec[i * kCRecordFloat4s * 4 + kCNodeFloats], &bvh.crefs[i * 4], 16);
+  }
+  const size_t b_cnodes = align256(crec.size() * 4);
   const size_t b_tris = align256(bvh.tris.size() * 4);
   const size_t b_shade = align256(bvh.tshade.size() * 4);
-  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_crefs;
+  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes;
 
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   if (ctx->scene_mem) {
@@ -444,9 +449,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     std::memcpy(host.data() + b_quads + b_sph + b_nodes, bvh.tris.data(), bvh.tris.size() * 4);
     std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris, bvh.tshade.data(),
                 bvh.tshade.size() * 4);
-    char* c = host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade;
-    std::memcpy(c, bvh.cnodes.data(), bvh.cnodes.size() * 4);
-    std::memcpy(c + b_cnodes, bvh.crefs.data(), bvh.crefs.size() * 4);
+    std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade, crec.data(), crec.size() * 4);
   }
   WGT_HIP(ctx, hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
 
@@ -458,7 +461,6 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.tris = (const float4*)(base + b_quads + b_sph + b_nodes);
   sc.tshade = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris);
   sc.cnodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade);
-  sc.crefs = (const int4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes);
   sc.cstep = bvh.cstep;
   sc.n_lights = n_lights;
   sc.n_quads = n_quads;
