@@ -132,15 +132,17 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.W = W;
   fr.H = H;
   fr.kernel = env_u32("WGT_KERNEL", 2);
-  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 10);  // swept on the persistent BVH4 kernel
-  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 8);
+  // swept on the persistent BVH4 kernel with compact nodes (DESIGN.md §4.2,
+  // profiles/sweeps/r01_sweep_compact_knobs.jsonl)
+  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 18);
+  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 16);
   fr.ps_svc_frac = env_u32("WGT_PS_SVC_FRAC", 16);  // sweep: profiles/sweeps/r01_ps_svc_frac.jsonl
   fr.tri_ratio = env_u32("WGT_TRI_RATIO", 100);
   fr.cnode = env_u32("WGT_CNODE", 2);  // compact nodes once the 128-B tree outgrows an XCD's L2
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
   fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
-  fr.pq_refill = env_u32("WGT_PQ_REFILL", 4);  // sweep: 2-4 best (profiles/sweeps)
+  fr.pq_refill = env_u32("WGT_PQ_REFILL", 2);  // sweep: 2-4 best (profiles/sweeps)
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   if (fr.pq_refill < 1) fr.pq_refill = 1;
