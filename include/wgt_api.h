@@ -134,6 +134,8 @@ typedef struct {
   uint32_t bvh_compact;   /* 1: the tree exceeds one XCD's L2 as 128-B nodes, so the persistent
                            * kernel reads its compact form (64-B nodes + 16-B refs) by default */
   float bvh_compact_step; /* scene-wide decode step of the compact nodes (wgt_geom.h) */
+  uint32_t ps_waves;      /* waves per SIMD of the persistent kernel: 6 when the tree collapses
+                           * under the 25-entry stack bound at <= 3% more nodes, else 5 */
 } wgt_scene_info;
 
 typedef struct wgt_ctx wgt_ctx;

@@ -204,3 +204,20 @@ def test_compact_nodes_full_size_meshes():
     for kind, compact in (("bunny", 0), ("sponza", 1)):
         tris = w.procedural_mesh(kind)
         assert check_compact(tris)["bvh_compact"] == compact
+
+
+def test_narrow_tree_selects_six_waves(monkeypatch):
+    """A tree that collapses under the 25-entry stack bound at <= 3% more nodes is
+    kept narrow, and the persistent kernel runs 6 waves per SIMD on it (bunny
+    stand-in: 17,791 vs 17,637 nodes); sponza's would grow 26%, so it keeps the
+    31-entry bound and 5 waves.  WGT_PS_WAVES=5 keeps every tree wide."""
+    bunny = w.procedural_mesh("bunny", 20000)
+    info = check_tree(bunny)  # the exported (= uploaded) tree passes the full walk
+    assert info["ps_waves"] == 6 and info["bvh_stack"] <= 25
+    for kind, waves in (("bunny", 6), ("sponza", 5)):
+        info, _, _ = w.bvh_build(w.procedural_mesh(kind))
+        assert info["ps_waves"] == waves
+        assert info["bvh_stack"] <= (25 if waves == 6 else 31)
+    monkeypatch.setenv("WGT_PS_WAVES", "5")
+    info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
+    assert info["ps_waves"] == 5 and info["bvh_stack"] == 31

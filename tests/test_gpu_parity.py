@@ -288,11 +288,13 @@ _SCHED_REF = {}
 @pytest.mark.parametrize("env", [{"WGT_PQ_LPT": "0"}, {"WGT_PQ_LPT": "1"}, {"WGT_PQ_REFILL": "1"},
                                  {"WGT_PQ_REFILL": "64"}, {"WGT_PS_TO_TRAV": "1", "WGT_PS_TO_SERVICE": "63"},
                                  {"WGT_PQ_LPT": "2"}, {"WGT_PS_SVC_FRAC": "0"}, {"WGT_PS_SVC_FRAC": "1"},
-                                 {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}])
+                                 {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
+                                 {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the
     cost pre-pass (1 or 4 spp) or block order; refill threshold; phase thresholds and
-    their sparse-wave scaling; the node form: compact nodes forced on the bunny)
+    their sparse-wave scaling; the node form: compact nodes forced on the bunny; the
+    bunny's narrow tree at 6 waves per SIMD or, with WGT_PS_WAVES=5, its wide one at 5)
     change which lane renders which pixel and when, never a bit of the result.  100x60
     leaves ragged 8x8 blocks at the frame edge.  The test runs after the kernel-family
     tests on the same context, the sequence that exposed a workspace-reuse bug (each

@@ -21,6 +21,7 @@ struct BvhOut {
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;  // BVH4 nodes / depth
   uint32_t n_nodes2 = 0, depth2 = 0;  // the SAH BVH2 the BVH4 was collapsed from
   uint32_t stack_need = 0;            // worst-case traversal stack entries (exact for this tree)
+  bool narrow = false;                // collapsed under narrow_limit (BuildBvh)
   double sah_cost = 0.0;
 };
 
@@ -28,7 +29,10 @@ struct BvhOut {
 // bounds the BVH4 depth and so the traversal stack (stack_need <= 3 * depth).
 // stack_limit bounds stack_need: a greedy collapse over the limit is redone
 // two-levels-per-node (stack_need <= 3 * ceil(depth2 / 2)).
+// narrow_limit > 0: the BVH2 is also collapsed under that smaller stack bound, and
+// that tree is kept (out.narrow) if it has at most kNarrowNodeRatio times the nodes.
+constexpr double kNarrowNodeRatio = 1.03;
 bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
-              BvhOut& out, std::string& err);
+              uint32_t narrow_limit, BvhOut& out, std::string& err);
 
 }  // namespace wgt

@@ -24,16 +24,15 @@ constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
 // at launch (dynamic LDS) to the builder's exact worst case DevScene::stack, so it
 // cannot overflow and needs no spill path.  kMaxBvhDepth bounds the SAH BVH2 the
 // BVH4 is collapsed from; kStackMax bounds the builder's stack need: + 1 parking
-// slot, so that LDS (160 KB per CU) admits kPsWaves waves per SIMD (4 SIMDs per
-// CU) on every scene: 5 waves -> 32 entries = 8 KB per wave, 6 -> 26 entries.
-// kPsWaves is also the register budget of k_render_ps (amdgpu_waves_per_eu).
-#ifndef WGT_PS_WAVES
-#define WGT_PS_WAVES 5
-#endif
-constexpr int kPsWaves = WGT_PS_WAVES;
+// slot, so that LDS (160 KB per CU) admits 5 waves per SIMD (4 SIMDs per CU):
+// 32 entries = 8 KB per wave.  A tree that collapses under kStackNarrow at
+// nearly the same size runs k_render_ps at 6 waves per SIMD instead (26 entries =
+// 6.5 KB per wave, 80 VGPRs): DevScene::ps_waves.
 constexpr int kMaxBvhDepth = 24;
-constexpr int kStackMax = (160 * 1024) / (kPsWaves * 4 * kBlock * 4) - 1;
-static_assert(kStackMax >= 16 && kStackMax <= 31, "stack bound out of the tested range");
+constexpr int kStackMax = 31;
+constexpr int kStackNarrow = 25;
+static_assert((kStackMax + 1) * kBlock * 4 * 5 * 4 <= 160 * 1024, "5 waves per SIMD");
+static_assert((kStackNarrow + 1) * kBlock * 4 * 6 * 4 <= 160 * 1024, "6 waves per SIMD");
 
 struct DevScene {
   const float4* __restrict__ quads;   // n_lights + n_quads records
@@ -48,6 +47,7 @@ struct DevScene {
   uint32_t last_sphere_emissive;
   float light_area;  // length(cross(lights[0].right, lights[0].up)) (path_tracer.wgsl:205)
   uint32_t stack;     // traversal stack entries per lane (>= 1)
+  uint32_t ps_waves;  // k_render_ps waves per SIMD: 6 for a tree built for kStackNarrow, else 5
 };
 // Dynamic LDS bytes of a traversal kernel launch.
 inline size_t stack_lds_bytes(const DevScene& sc) { return (size_t)sc.stack * kBlock * sizeof(int); }

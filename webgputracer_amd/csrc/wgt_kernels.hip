@@ -103,8 +103,8 @@ constexpr uint32_t kCostService = 7;  // a service iteration ~ 7 traversal steps
     if (STATS) acc += __builtin_amdgcn_s_memtime() - r0_;     \
   } while (0)
 
-template <bool STATS, bool COST, bool CN>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kPsWaves)))
+template <bool STATS, bool COST, bool CN, int W>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
             unsigned long long* __restrict__ counters, uint32_t* __restrict__ queue) {
@@ -376,6 +376,20 @@ hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d
 // k_render_ps reads the compact nodes when asked to, or by default when the 128-B
 // tree would not fit one XCD's 4 MB L2 (sponza stand-in: 8.5 MB -> 4.3 + 1.1 MB);
 // a tree that fits keeps the 128-B nodes, whose step needs fewer VALU.
+// k_render_ps at the scene's waves per SIMD and node form.
+template <bool STATS, bool COST>
+void ps_launch(const DevScene& sc, bool cn, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
+               const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
+               uint32_t* queue) {
+  if (sc.ps_waves == 6) {
+    if (cn) k_render_ps<STATS, COST, true, 6><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+    else k_render_ps<STATS, COST, false, 6><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+  } else {
+    if (cn) k_render_ps<STATS, COST, true, 5><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+    else k_render_ps<STATS, COST, false, 5><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+  }
+}
+
 bool use_compact_nodes(const DevScene& sc, const DevFrame& fr) {
   return fr.cnode == 1 || (fr.cnode == 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes);
 }
@@ -419,20 +433,14 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       fc.inv_fspp = pow2_recip(fc.sqrt_spp * fc.sqrt_spp);
       fc.cost = (uint32_t*)((char*)ws + 256);
       fc.n_slots = nb * 16u;  // a quarter of each block's pixels estimate its cost
-      if (cn) k_render_ps<false, true, true><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
-      else k_render_ps<false, true, false><<<grid, block, lds, stream>>>(sc, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
+      ps_launch<false, true>(sc, cn, grid, block, lds, stream, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
       k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb);
       f.perm = fc.cost + nb;
       e = hipGetLastError();
     }
     if (e == hipSuccess) {
-      if (counters) {
-        if (cn) k_render_ps<true, false, true><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, counters, q + 1);
-        else k_render_ps<true, false, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, counters, q + 1);
-      } else {
-        if (cn) k_render_ps<false, false, true><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
-        else k_render_ps<false, false, false><<<grid, block, lds, stream>>>(sc, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
-      }
+      if (counters) ps_launch<true, false>(sc, cn, grid, block, lds, stream, f, d_tiles, out8, out32, outhit, counters, q + 1);
+      else ps_launch<false, false>(sc, cn, grid, block, lds, stream, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
       e = hipGetLastError();
     }
     return e;
@@ -449,10 +457,16 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
 }
 
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
-  const void* variants[4] = {reinterpret_cast<const void*>(&k_render_ps<false, false, false>),
-                             reinterpret_cast<const void*>(&k_render_ps<true, false, false>),
-                             reinterpret_cast<const void*>(&k_render_ps<false, false, true>),
-                             reinterpret_cast<const void*>(&k_render_ps<true, false, true>)};
+  const bool w6 = sc.ps_waves == 6;
+  const void* variants[4] = {
+      w6 ? reinterpret_cast<const void*>(&k_render_ps<false, false, false, 6>)
+         : reinterpret_cast<const void*>(&k_render_ps<false, false, false, 5>),
+      w6 ? reinterpret_cast<const void*>(&k_render_ps<true, false, false, 6>)
+         : reinterpret_cast<const void*>(&k_render_ps<true, false, false, 5>),
+      w6 ? reinterpret_cast<const void*>(&k_render_ps<false, false, true, 6>)
+         : reinterpret_cast<const void*>(&k_render_ps<false, false, true, 5>),
+      w6 ? reinterpret_cast<const void*>(&k_render_ps<true, false, true, 6>)
+         : reinterpret_cast<const void*>(&k_render_ps<true, false, true, 5>)};
   // the largest of the variants' capacities: waves beyond a variant's capacity
   // start as others retire and find the queue drained or nearly so
   int per_cu = 0, cus = 0;

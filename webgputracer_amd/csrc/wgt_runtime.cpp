@@ -102,6 +102,8 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 // operations as the WGSL per-invocation evaluation.
 // The builder's stack bound (WGT_STACK_LIMIT overrides kStackMax for sweeps).
 uint32_t stack_limit() { return std::min(env_u32("WGT_STACK_LIMIT", (uint32_t)kStackMax), (uint32_t)kStackMax); }
+// The narrow collapse for 6 waves per SIMD (WGT_PS_WAVES=5 keeps every tree at 5).
+uint32_t narrow_limit() { return env_u32("WGT_PS_WAVES", 0) == 5 ? 0u : (uint32_t)kStackNarrow; }
 
 DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   DevFrame fr{};
@@ -361,7 +363,7 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   if (!tris || n_tris == 0 || !info) return fail(nullptr, WGT_E_INVALID, "null triangles or info");
   BvhOut bvh;
   std::string err;
-  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), bvh, err))
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), bvh, err))
     return fail(nullptr, WGT_E_INVALID, err);
   *info = wgt_scene_info{};
   info->n_tris = n_tris;
@@ -382,6 +384,7 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   if (tris_out) std::memcpy(tris_out, bvh.tris.data(), bvh.tris.size() * 4);
   info->bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
   info->bvh_compact_step = bvh.cstep;
+  info->ps_waves = bvh.narrow ? 6u : 5u;
   return WGT_OK;
 }
 
@@ -391,7 +394,7 @@ int wgt_bvh_build_compact(const wgt_triangle* tris, uint32_t n_tris, uint32_t* c
     return fail(nullptr, WGT_E_INVALID, "null triangles or outputs");
   BvhOut bvh;
   std::string err;
-  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), bvh, err))
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), bvh, err))
     return fail(nullptr, WGT_E_INVALID, err);
   if (nodes_cap < bvh.n_nodes) return fail(nullptr, WGT_E_INVALID, "node capacity too small");
   std::memcpy(cnodes_out, bvh.cnodes.data(), bvh.cnodes.size() * 4);
@@ -415,7 +418,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   BvhOut bvh;
   if (n_tris > 0) {
     std::string err;
-    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), bvh, err)) return fail(ctx, WGT_E_INVALID, err);
+    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), bvh, err)) return fail(ctx, WGT_E_INVALID, err);
   }
   const uint32_t nlq = n_lights + n_quads;
   const size_t b_quads = align256((size_t)nlq * 96);
@@ -475,6 +478,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
   // + 1: the speculative traversal parks a second leaf on the stack (wgt_device.h)
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
+  sc.ps_waves = bvh.narrow ? 6u : 5u;
   WGT_HIP(ctx, ps_resident_waves(sc, ctx->device, ctx->ps_resident));
 
   wgt_scene_info& in = ctx->info;
@@ -495,6 +499,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   in.bvh2_depth = bvh.depth2;
   in.bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
   in.bvh_compact_step = bvh.cstep;
+  in.ps_waves = n_tris ? sc.ps_waves : 0u;
   ctx->has_scene = true;
   return WGT_OK;
 }
