@@ -64,6 +64,9 @@ def main():
             out.append(f"| `{k}` | {c} | {v:,.1f} |")
     sys.path.insert(0, ROOT)
     timed = line["per_launch"]["kernel"]
+    if not any(k == timed for k, _ in per):  # older bench lines name fewer template arguments
+        cand = sorted({k for k, _ in per if k.startswith(timed[:-1] + ",")})
+        timed = cand[0] if len(cand) == 1 else timed
     fetch = per.get((timed, "FETCH_SIZE"))
     write = per.get((timed, "WRITE_SIZE"))
     if fetch is not None and write is not None:
