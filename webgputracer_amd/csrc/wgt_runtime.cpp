@@ -136,8 +136,9 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.kernel = env_u32("WGT_KERNEL", 2);
   // swept on the persistent BVH4 kernel with compact nodes (DESIGN.md §4.2,
   // profiles/sweeps/r01_sweep_compact_knobs.jsonl)
-  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 18);
-  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 16);
+  // 0 = by the kernel's waves per SIMD: 18/16 at 5, 16/14 at 6 (launch_render)
+  fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 0);
+  fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 0);
   fr.ps_svc_frac = env_u32("WGT_PS_SVC_FRAC", 16);  // sweep: profiles/sweeps/r01_ps_svc_frac.jsonl
   fr.tri_ratio = env_u32("WGT_TRI_RATIO", 100);
   fr.cnode = env_u32("WGT_CNODE", 2);  // compact nodes once the 128-B tree outgrows an XCD's L2
