@@ -287,7 +287,8 @@ _SCHED_REF = {}
 
 @pytest.mark.parametrize("env", [{"WGT_PQ_LPT": "0"}, {"WGT_PQ_LPT": "1"}, {"WGT_PQ_REFILL": "1"},
                                  {"WGT_PQ_REFILL": "64"}, {"WGT_PS_TO_TRAV": "1", "WGT_PS_TO_SERVICE": "63"},
-                                 {"WGT_PQ_LPT": "2"}, {"WGT_PS_SVC_FRAC": "0"}, {"WGT_PS_SVC_FRAC": "1"},
+                                 {"WGT_PQ_LPT": "2"}, {"WGT_PQ_LPT_ALL": "0"}, {"WGT_PS_SVC_FRAC": "0"},
+                                 {"WGT_PS_SVC_FRAC": "1"},
                                  {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
                                  {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):

@@ -92,6 +92,7 @@ struct DevFrame {
   // the queue order (queue block q renders pixel block perm[q]; NULL = identity)
   // and the pre-pass cost per pixel block (set by launch_render)
   uint32_t n_slots, pq_refill, pq_lpt;
+  uint32_t pq_lpt_all;  // the pre-pass renders all 64 pixels of each block (else the 16 at even x, y)
   const uint32_t* perm;
   uint32_t* cost;
 

@@ -92,7 +92,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
 // coordinates and seed: which lane or wave computes it does not change a bit.
 // COST: the 1-spp pre-pass: no output, each finished pixel adds its work units
 // (kCostService per ray started + 1 per traversal step) to fr.cost[its block];
-// it renders the 16 pixels at even (x, y) of each 8x8 block.
+// it renders every pixel of each 8x8 block (fr.pq_lpt_all) or the 16 at even (x, y).
 constexpr uint32_t kCostService = 7;  // a service iteration ~ 7 traversal steps (profiles/)
 // STATS: wave cycles per service-phase region (s_memtime; the regions run in
 // divergent code, so each adds the wave's time spent issuing or waiting in it).
@@ -162,8 +162,9 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
               exhausted = true;
             } else {
               // COST pre-pass: 16 slots per block, the pixels at even (x, y) of the 8x8 block
-              const uint32_t sb = COST ? (slot >> 4) : (slot >> 6);
-              const uint32_t sl = COST ? (((slot & 3u) << 1) | (((slot >> 2) & 3u) << 4)) : (slot & 63u);
+              const bool quarter = COST && !fr.pq_lpt_all;
+              const uint32_t sb = quarter ? (slot >> 4) : (slot >> 6);
+              const uint32_t sl = quarter ? (((slot & 3u) << 1) | (((slot >> 2) & 3u) << 4)) : (slot & 63u);
               const uint32_t b = fr.perm ? fr.perm[sb] : sb;
               if (slot_setup(fr, tiles, b, sl, po, px)) {
                 have = true;
@@ -435,7 +436,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       fc.fspp = (float)(fc.sqrt_spp * fc.sqrt_spp);
       fc.inv_fspp = pow2_recip(fc.sqrt_spp * fc.sqrt_spp);
       fc.cost = (uint32_t*)((char*)ws + 256);
-      fc.n_slots = nb * 16u;  // a quarter of each block's pixels estimate its cost
+      fc.n_slots = nb * (fr.pq_lpt_all ? 64u : 16u);  // by default a quarter of each block's pixels estimate its cost
       ps_launch<false, true>(sc, cn, grid, block, lds, stream, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
       k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb);
       f.perm = fc.cost + nb;
