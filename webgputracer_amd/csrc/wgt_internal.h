@@ -93,6 +93,7 @@ struct DevFrame {
   // and the pre-pass cost per pixel block (set by launch_render)
   uint32_t n_slots, pq_refill, pq_lpt;
   uint32_t pq_lpt_all;  // the pre-pass renders all 64 pixels of each block (else the 16 at even x, y)
+  uint32_t pq_svc_cost;  // pre-pass work units per ray started (a service iteration ~ 7 traversal steps)
   const uint32_t* perm;
   uint32_t* cost;
 

@@ -91,9 +91,8 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
 // slots are one 8x8 pixel block.  Each pixel's result depends only on its
 // coordinates and seed: which lane or wave computes it does not change a bit.
 // COST: the 1-spp pre-pass: no output, each finished pixel adds its work units
-// (kCostService per ray started + 1 per traversal step) to fr.cost[its block];
+// (fr.pq_svc_cost per ray started + 1 per traversal step) to fr.cost[its block];
 // it renders every pixel of each 8x8 block (fr.pq_lpt_all) or the 16 at even (x, y).
-constexpr uint32_t kCostService = 7;  // a service iteration ~ 7 traversal steps (profiles/)
 // STATS: wave cycles per service-phase region (s_memtime; the regions run in
 // divergent code, so each adds the wave's time spent issuing or waiting in it).
 #define WGT_REGION(acc, ...)                                  \
@@ -232,7 +231,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           Hit h;
           WGT_REGION(cr_quads, quad_scan(sc, ro, rd, h, q_t); q_prim = h.prim;
                      trav_init(ro, rd, q_prim != kNoHit, q_t, t));
-          if (COST) work += kCostService;
+          if (COST) work += fr.pq_svc_cost;
           // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
           WGT_REGION(cr_root, node_step<STATS, CN>(sc, t, lds, st));

@@ -148,6 +148,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.pq_refill = env_u32("WGT_PQ_REFILL", 2);  // sweep: 2-4 best (profiles/sweeps)
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
+  fr.pq_svc_cost = env_u32("WGT_PQ_SVC_COST", 7);
   fr.pq_lpt_all = env_u32("WGT_PQ_LPT_ALL", 1);  // sweep: all pixels -3% (sponza), -4% (bunny) at 256 spp
   if (fr.pq_refill < 1) fr.pq_refill = 1;
   return fr;
