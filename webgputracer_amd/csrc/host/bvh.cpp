@@ -385,7 +385,7 @@ float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes) {
 }  // namespace
 
 bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
-              uint32_t narrow_limit, BvhOut& out, std::string& err) {
+              uint32_t narrow_limit, double narrow_ratio, BvhOut& out, std::string& err) {
   out = BvhOut{};
   if (n == 0) { err = "BuildBvh: no triangles"; return false; }
   if (n >= (1u << 28)) { err = "BuildBvh: too many triangles (max 2^28-1)"; return false; }
@@ -450,7 +450,7 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
     Collapser tight(n2, nar);
     tight.Collapse(0, 0, narrow_limit, nar.stack_need);
     const uint32_t nn = (uint32_t)(nar.nodes.size() / kNode4Floats);
-    if (nar.stack_need <= narrow_limit && nn <= kNarrowNodeRatio * out.n_nodes) {
+    if (nar.stack_need <= narrow_limit && nn <= narrow_ratio * out.n_nodes) {
       out.nodes.swap(nar.nodes);
       out.n_nodes = nn;
       out.stack_need = nar.stack_need;

@@ -30,9 +30,9 @@ struct BvhOut {
 // stack_limit bounds stack_need: a greedy collapse over the limit is redone
 // two-levels-per-node (stack_need <= 3 * ceil(depth2 / 2)).
 // narrow_limit > 0: the BVH2 is also collapsed under that smaller stack bound, and
-// that tree is kept (out.narrow) if it has at most kNarrowNodeRatio times the nodes.
+// that tree is kept (out.narrow) if it has at most narrow_ratio times the nodes.
 constexpr double kNarrowNodeRatio = 1.03;
 bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
-              uint32_t narrow_limit, BvhOut& out, std::string& err);
+              uint32_t narrow_limit, double narrow_ratio, BvhOut& out, std::string& err);
 
 }  // namespace wgt

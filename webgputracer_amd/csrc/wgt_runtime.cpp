@@ -102,8 +102,10 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 // operations as the WGSL per-invocation evaluation.
 // The builder's stack bound (WGT_STACK_LIMIT overrides kStackMax for sweeps).
 uint32_t stack_limit() { return std::min(env_u32("WGT_STACK_LIMIT", (uint32_t)kStackMax), (uint32_t)kStackMax); }
-// The narrow collapse for 6 waves per SIMD (WGT_PS_WAVES=5 keeps every tree at 5).
+// The narrow collapse for 6 waves per SIMD: WGT_PS_WAVES=5 keeps every tree at 5,
+// 6 takes the narrow tree whenever the BVH2 is shallow enough (sweeps).
 uint32_t narrow_limit() { return env_u32("WGT_PS_WAVES", 0) == 5 ? 0u : (uint32_t)kStackNarrow; }
+double narrow_ratio() { return env_u32("WGT_PS_WAVES", 0) == 6 ? 1e30 : kNarrowNodeRatio; }
 
 DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   DevFrame fr{};
@@ -366,7 +368,7 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   if (!tris || n_tris == 0 || !info) return fail(nullptr, WGT_E_INVALID, "null triangles or info");
   BvhOut bvh;
   std::string err;
-  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), bvh, err))
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(), bvh, err))
     return fail(nullptr, WGT_E_INVALID, err);
   *info = wgt_scene_info{};
   info->n_tris = n_tris;
@@ -397,7 +399,7 @@ int wgt_bvh_build_compact(const wgt_triangle* tris, uint32_t n_tris, uint32_t* c
     return fail(nullptr, WGT_E_INVALID, "null triangles or outputs");
   BvhOut bvh;
   std::string err;
-  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), bvh, err))
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(), bvh, err))
     return fail(nullptr, WGT_E_INVALID, err);
   if (nodes_cap < bvh.n_nodes) return fail(nullptr, WGT_E_INVALID, "node capacity too small");
   std::memcpy(cnodes_out, bvh.cnodes.data(), bvh.cnodes.size() * 4);
@@ -421,7 +423,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   BvhOut bvh;
   if (n_tris > 0) {
     std::string err;
-    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), bvh, err)) return fail(ctx, WGT_E_INVALID, err);
+    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(), bvh, err)) return fail(ctx, WGT_E_INVALID, err);
   }
   const uint32_t nlq = n_lights + n_quads;
   const size_t b_quads = align256((size_t)nlq * 96);
