@@ -152,7 +152,6 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   fr.pq_svc_cost = env_u32("WGT_PQ_SVC_COST", 7);
   fr.pq_lpt_all = env_u32("WGT_PQ_LPT_ALL", 1);  // sweep: all pixels -3% (sponza), -4% (bunny) at 256 spp
-  if (fr.pq_refill < 1) fr.pq_refill = 1;
   return fr;
 }
 
