@@ -250,6 +250,24 @@ def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
     assert info["bvh_compact"] == 1
 
 
+@pytest.mark.parametrize("kind,spp", [("sponza", 4), ("bunny", 1)])
+def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp):
+    """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
+    oracle (OpenMP), through the default kernel of each scene: sponza on the compact
+    nodes at 5 waves/SIMD, bunny on the narrow 128-B tree at 6."""
+    L, Q, S, T = wgt.mesh_scene(kind)
+    ctx.upload_scene(L, Q, S, T)
+    info = ctx.scene_info()
+    assert (info["bvh_compact"], info["ps_waves"]) == ((1, 5) if kind == "sponza" else (0, 6))
+    osc = oracle.OracleScene(L, Q, S, T)
+    g = ctx.render_tile(wgt.camera_param(16 / 9, spp, 3), 1920, 1080, stats=True)
+    r = osc.render(oracle.camera_param(16 / 9, spp, 3), 1920, 1080)
+    osc.close()
+    assert_radiance(g["f32"], r["f32"])
+    assert np.array_equal(g["hit"], r["hit"])
+    check_counters(g["stats"], r["counters"], oracle)
+
+
 def test_sponza_1080p_256spp_subsample_compact(ctx, wgt, oracle):
     """BASELINE config 4 (the bench workload) at full size through the compact nodes:
     GPU tiles of the 1920x1080/256spp frame vs the oracle on the same global pixels."""
