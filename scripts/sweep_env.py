@@ -13,7 +13,7 @@ import webgputracer_amd as w  # noqa: E402
 scene, W, H, spp = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4])
 envs = [e for e in sys.argv[5].split(";")]
 ctx = w.Context(0)
-ctx.upload_scene(*w.mesh_scene(scene))
+ctx.upload_scene(*(w.cornell_scene() if scene == "cornell" else w.mesh_scene(scene)))
 cam = w.camera_param(W / H, spp, 0)
 ref = None
 base = dict(os.environ)
@@ -24,7 +24,7 @@ for env in envs:
         k, v = kv.split("=")
         os.environ[k] = v
     if os.environ.get("REUPLOAD"):  # builder knobs: rebuild the BVH under this env
-        ctx.upload_scene(*w.mesh_scene(scene))
+        ctx.upload_scene(*(w.cornell_scene() if scene == "cornell" else w.mesh_scene(scene)))
     runs = [ctx.render_tile(cam, W, H, want=("u8",), stats=True) for _ in range(int(os.environ.get("REPS", "2")))]
     st = runs[0]["stats"]
     same = ref is None or np.array_equal(runs[0]["u8"], ref)

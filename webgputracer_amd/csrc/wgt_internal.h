@@ -31,6 +31,8 @@ constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
 constexpr int kMaxBvhDepth = 24;
 constexpr int kStackMax = 31;
 constexpr int kStackNarrow = 25;
+// k_render_ps on scenes without triangles (no traversal, no stack): its register budget
+constexpr int kPsWavesNoTris = 8;
 static_assert((kStackMax + 1) * kBlock * 4 * 5 * 4 <= 160 * 1024, "5 waves per SIMD");
 static_assert((kStackNarrow + 1) * kBlock * 4 * 6 * 4 <= 160 * 1024, "6 waves per SIMD");
 

@@ -102,7 +102,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
     if (STATS) acc += __builtin_amdgcn_s_memtime() - r0_;     \
   } while (0)
 
-template <bool STATS, bool COST, bool CN, int W>
+template <bool STATS, bool COST, bool CN, int W, bool TRIS = true>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
@@ -234,9 +234,13 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           if (COST) work += fr.pq_svc_cost;
           // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
-          WGT_REGION(cr_root, node_step<STATS, CN>(sc, t, lds, st));
-          if (trav_done(t)) pending = true;
-          else trav = true;
+          if (TRIS) {
+            WGT_REGION(cr_root, node_step<STATS, CN>(sc, t, lds, st));
+            if (trav_done(t)) pending = true;
+            else trav = true;
+          } else {
+            pending = true;  // no triangles: the quad and sphere scans are the whole query
+          }
           break;
         }
       }
@@ -255,7 +259,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       const uint32_t sparse = (live * fr.ps_svc_frac) >> 6;
       to_service = sparse < to_service ? sparse : to_service;
     }
-    for (;;) {
+    for (; TRIS;) {
       // one uniform mode per step: triangle steps once enough lanes hold a
       // pending leaf (weighted by the two steps' costs), else node steps
       const bool can_node = trav && t.ref != kNoRef;
@@ -381,7 +385,9 @@ template <bool STATS, bool COST>
 void ps_launch(const DevScene& sc, bool cn, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
                const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
                uint32_t* queue) {
-  if (sc.ps_waves == 6) {
+  if (sc.n_tris == 0) {
+    k_render_ps<STATS, COST, false, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+  } else if (sc.ps_waves == 6) {
     if (cn) k_render_ps<STATS, COST, true, 6><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
     else k_render_ps<STATS, COST, false, 6><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
   } else {
@@ -410,7 +416,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   const dim3 block(kBlock);
   const size_t lds = stack_lds_bytes(sc);
   const bool tris = sc.n_tris > 0;
-  if (tris && fr.kernel == 2) {
+  if (fr.kernel == 2) {
     if (blocks * 64ull > 0xffffffffull || resident == 0) return hipErrorInvalidValue;
     if (!ws || ws_cap < render_ws_bytes(fr)) return hipErrorInvalidValue;
     const uint32_t nb = (uint32_t)blocks;
@@ -462,6 +468,8 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
 
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
   const bool w6 = sc.ps_waves == 6;
+  const void* notris[2] = {reinterpret_cast<const void*>(&k_render_ps<false, false, false, kPsWavesNoTris, false>),
+                           reinterpret_cast<const void*>(&k_render_ps<true, false, false, kPsWavesNoTris, false>)};
   const void* variants[4] = {
       w6 ? reinterpret_cast<const void*>(&k_render_ps<false, false, false, 6>)
          : reinterpret_cast<const void*>(&k_render_ps<false, false, false, 5>),
@@ -475,6 +483,14 @@ hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
   // start as others retire and find the queue drained or nearly so
   int per_cu = 0, cus = 0;
   for (const void* k : variants) {
+    if (sc.n_tris == 0) break;
+    int n = 0;
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, stack_lds_bytes(sc));
+    if (e != hipSuccess) return e;
+    per_cu = n > per_cu ? n : per_cu;
+  }
+  for (const void* k : notris) {
+    if (sc.n_tris != 0) break;
     int n = 0;
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, stack_lds_bytes(sc));
     if (e != hipSuccess) return e;
