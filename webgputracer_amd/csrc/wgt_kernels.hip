@@ -10,9 +10,9 @@
 // stack, Moller-Trumbore in fp32, wgt_geom.h), then the sphere scan.
 //
 // Two kernels compute bit-identical results:
-//  * k_render (simple): a flat per-lane loop, one closest-hit query + one shading
-//    step per iteration.  Used for scenes without triangles (the Cornell box).
-//  * k_render_ps (phase-split, scenes with triangles): the wave alternates a
+//  * k_render (simple, WGT_KERNEL=1): a flat per-lane loop, one closest-hit query +
+//    one shading step per iteration.
+//  * k_render_ps (persistent, the default): the wave alternates a
 //    SERVICE phase (finalise the hit of lanes whose traversal ended, shade, start
 //    the next ray: camera ray or bounce, quad scan, root-node test) and a
 //    TRAVERSAL phase (one BVH node or leaf per lane per step).  A phase ends when
@@ -20,6 +20,8 @@
 //    ray left the BVH early pick up new rays while the long traversals continue:
 //    the traversal loop runs at 10 % SIMT utilisation in k_render on the bunny
 //    stand-in (profiles/r01_*), which this structure removes.
+//    Without triangles (TRIS = false, the Cornell box) there is no traversal phase:
+//    the persistent pixel queue alone balances the pixels.
 //
 // NaN rays (any NaN in start/dir) are resolved without tracing: every rejection
 // test of the reference is false for NaN, so the last primitive of the scan — the
