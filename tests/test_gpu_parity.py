@@ -5,6 +5,8 @@ triangle/primitive IDs bit-exact.  The kernels are built to reproduce the oracle
 fp32 evaluation exactly, so these tests demand bit equality of the float32
 radiance (the 1e-4 relative check is asserted too, as the contractual bar).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -258,7 +260,8 @@ def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp):
     L, Q, S, T = wgt.mesh_scene(kind)
     ctx.upload_scene(L, Q, S, T)
     info = ctx.scene_info()
-    assert (info["bvh_compact"], info["ps_waves"]) == ((1, 5) if kind == "sponza" else (0, 6))
+    if not any(os.environ.get(k) for k in ("WGT_CNODE", "WGT_PS_WAVES", "WGT_STACK_LIMIT")):  # the defaults
+        assert (info["bvh_compact"], info["ps_waves"]) == ((1, 5) if kind == "sponza" else (0, 6))
     osc = oracle.OracleScene(L, Q, S, T)
     g = ctx.render_tile(wgt.camera_param(16 / 9, spp, 3), 1920, 1080, stats=True)
     r = osc.render(oracle.camera_param(16 / 9, spp, 3), 1920, 1080)
