@@ -42,9 +42,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 NODE_BYTES, CNODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 48, 32
 
 
-def dominant_kernel(compact: bool, waves: int) -> str:
-    """The timed k_render_ps instantiation <STATS, COST, compact nodes, waves per SIMD>."""
-    return f"wgt::k_render_ps<false, false, {'true' if compact else 'false'}, {waves}>"
+def dominant_kernel(compact: bool, waves: int, tris: bool = True) -> str:
+    """The timed k_render_ps instantiation <STATS, COST, compact nodes, waves per SIMD, triangles>
+    (a scene without triangles runs the 8-wave instantiation without traversal)."""
+    if not tris:
+        return "wgt::k_render_ps<false, false, false, 8, false>"
+    return f"wgt::k_render_ps<false, false, {'true' if compact else 'false'}, {waves}, true>"
 
 
 def compact_nodes(info) -> bool:
@@ -228,7 +231,7 @@ def main():
     if rank == 0:
         # dominant kernel = k_render_ps; algorithmic bytes of rank 0's launch
         compact = compact_nodes(info)
-        kernel = dominant_kernel(compact, int(info.get("ps_waves", 5)))
+        kernel = dominant_kernel(compact, int(info.get("ps_waves", 5)), info["n_tris"] > 0)
         node_b = CNODE_BYTES if compact else NODE_BYTES
         bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
