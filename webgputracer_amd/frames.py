@@ -3,10 +3,14 @@ rendered by one process per GPU, frames dealt round-robin, no collective.
 
 Replaces the reference's machine split (settings/run.py:11-24: frames 1-320 on
 one host, 321-600 on another, each running `WebGPUTracer --frame s e`,
-main.cpp:17-33) inside one node: rank r of N renders the frames f with
-(f - start) % N == r.  The camera is static (Camera::Update ignores t,
-camera.cpp:64-70), so frames differ only by their seed: seed = frame index
-(SURVEY A23; the reference draws std::random_device, util.h:43-47).
+main.cpp:17-33) inside one node.  `--frame s e` means the frames
+i = s-1 ... e-1 written as "%03d.png" % i (Renderer::OnCompute's loop
+`for (i = start_frame - 1; i < end_frame; ++i) OnRender(i)`, render.cpp:437-439,
+and the file name of OnRender, render.cpp:493-497), so `--frame 1 600` writes
+000.png ... 599.png; rank r of N renders the frames i with (i - (s-1)) % N == r.
+The camera is static (Camera::Update ignores t, camera.cpp:64-70), so frames
+differ only by their seed: seed = frame index i (the reference draws
+std::random_device, util.h:43-47; the C++ CLI's --fixed-seed uses the same i).
 
 Frames are rendered B per launch (wgt_render_frames: one full-frame tile per
 frame, each with its frame's seed), so the persistent kernel's end-of-launch
@@ -29,11 +33,18 @@ import numpy as np
 from .tracer import Context, camera_param, cornell_scene, mesh_scene, write_png
 
 
-def frames_of_rank(start: int, end: int, rank: int, world: int):
-    """Frames [start, end] of `rank`: round-robin, as even as the range allows."""
-    if end < start:
+def frame_indices(start: int, end: int):
+    """The frame indices `--frame start end` renders: start-1 ... end-1
+    (render.cpp:437, `for (uint32_t i = start_frame - 1; i < end_frame; ++i)`)."""
+    if start < 1 or end < start:
         return []
-    return [f for f in range(start, end + 1) if (f - start) % world == rank]
+    return list(range(start - 1, end))
+
+
+def frames_of_rank(start: int, end: int, rank: int, world: int):
+    """Frame indices of `--frame start end` (frame_indices) dealt to `rank`:
+    round-robin, as even as the range allows."""
+    return [f for k, f in enumerate(frame_indices(start, end)) if k % world == rank]
 
 
 def batches(frames, batch: int):
@@ -65,6 +76,8 @@ def main(argv=None):
                     help="frames per launch (8: 30.9 frames/s vs 30.2 at 4, profiles/configs/r01j_c5_frames.jsonl)")
     ap.add_argument("--out", default=None, help="directory for NNN.png (none: render only)")
     a = ap.parse_args(argv)
+    if a.frame[0] < 1 or a.frame[1] < a.frame[0]:
+        ap.error("bad frame range")  # the C++ CLI's check (csrc/main.cpp)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
