@@ -151,42 +151,27 @@ def main():
 
     # this step's frames (frame id, seed): one per GPU (weak scaling) or one in all (strong)
     frames = [(j, j) for j in range(world)] if args.scaling == "weak" else [(0, 0)]
-    tiles = wdist.shard_tiles(W, H, T, frames, rank, world)
-    n_max = wdist.max_tiles_per_rank(W, H, T, len(frames), world)
     dev = torch.device("cuda", local)
-    d_tiles = torch.from_numpy(tiles.view(np.uint8).copy()).to(dev)
-    out = torch.zeros((n_max, T, T, 4), dtype=torch.uint8, device=dev)
     cam = w.camera_param(W / H, spp, 0)  # per-tile seeds override cam.seed
+    # the rank's tiles, its compact output buffer and (rank 0) the assembly index, all resident
+    shard = wdist.ShardedFrames(ctx, cam, W, H, T, frames, rank, world, dist, dev, backend=args.dist_backend)
 
     # instrumented pass (untimed): exact counts for this rank's tiles
-    st = ctx.render_tiles_stats(cam, W, H, T, T, d_tiles.data_ptr(), len(tiles))
+    st = shard.stats()
 
     # a real (non-NULL) stream: the launch, the events and the gather are ordered on it
     stream = torch.cuda.Stream(device=dev)
     torch.cuda.set_stream(stream)
-
-    # rank 0 assembles the step's frames with one gather op (index built once, here)
     frame_ids = [f for f, _ in frames]
-    if world == 1:
-        layout = tiles
-    else:
-        layout = np.concatenate([wdist.pad_tiles(wdist.shard_tiles(W, H, T, frames, r, world), n_max)
-                                 for r in range(world)])
-    asm_idx = torch.from_numpy(wdist.assemble_index(layout, W, H, T, frame_ids)).to(dev) if rank == 0 else None
 
     def step(ev):
         if ev is not None:
             ev[0].record(stream)
-        ctx.render_tiles_async(cam, W, H, T, T, d_tiles.data_ptr(), len(tiles), d_u8=out.data_ptr(),
-                               stream=stream.cuda_stream)
+        shard.launch(stream.cuda_stream)
         if ev is not None:
             ev[1].record(stream)
-        bufs = wdist.gather_tiles(out if args.dist_backend == "nccl" else out.cpu(), rank, world, dist)
-        if rank == 0:
-            data = (bufs[0] if world == 1 else torch.cat(bufs)).to(dev).reshape(-1, 4)
-            imgs = data[asm_idx]  # (frames, H, W, 4)
-            return {f: imgs[i] for i, f in enumerate(frame_ids)}
-        return None
+        got = shard.gather()
+        return got["u8"] if got is not None else None
 
     for _ in range(args.warmup):
         step(None)

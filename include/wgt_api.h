@@ -191,9 +191,13 @@ int wgt_render_frames(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uin
 
 /* Tile-list launch with DEVICE buffers: n_tiles tiles of tw x th (d_tiles: device
  * array of wgt_tile) written compactly, tile after tile (out[(t*th + ly)*tw + lx]).
- * cam->seed is ignored (per-tile seeds).  Asynchronous for megakernel scenes; for
- * scenes with triangles the wavefront loop polls a device completion counter, so
- * the call returns when the frame is done (work is ordered on `stream`). */
+ * cam->seed is ignored (per-tile seeds).  Always asynchronous: the call returns
+ * as soon as the launches are queued, ordered on `stream`, and after every earlier
+ * launch of the same context on any stream; read the outputs only after
+ * synchronising `stream`.  The one exception is the wavefront kernel family
+ * (WGT_KERNEL=0, off by default), whose host loop polls a device completion
+ * counter and returns when the frame is done.  wgt_upload_scene and wgt_destroy
+ * wait for every launch of the context before freeing what it reads. */
 int wgt_render_tiles_async(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint32_t H,
                            uint32_t tw, uint32_t th, const wgt_tile *d_tiles, uint32_t n_tiles,
                            void *d_rgba8, float *d_rgba32f, uint32_t *d_hit_id, void *stream);
@@ -216,11 +220,16 @@ int wgt_trace_rays_async(wgt_ctx *ctx, const float *d_rays, uint32_t n, uint32_t
                          float *d_dist, void *stream);
 
 int wgt_sync(wgt_ctx *ctx);
-/* Diagnostics: the kernels' short correctly-rounded sqrt / division sequences
- * (wgt_math.h sqrt_rn, div_rn) against the IEEE operations on n pseudo-random
- * inputs per operation from the ranges the kernels feed them; counts[0..3] =
- * sqrt tests, sqrt mismatches, div tests, div mismatches (synchronous). */
-int wgt_selftest_math(wgt_ctx *ctx, uint32_t n, uint32_t seed, uint64_t counts[4]);
+/* Diagnostics: the kernels' short sqrt / division forms (wgt_math.h sqrt_rn,
+ * sqrt_fast, div_rn) against correctly rounded results (the f64 operation rounded
+ * to f32): sqrt_rn on all 2^32 inputs, sqrt_fast on every input of its domain,
+ * div_rn on n pseudo-random operand pairs of the quad distance under the render
+ * limits (accept decision and accepted bits).  counts[0..7] = sqrt tests (2^32),
+ * sqrt_rn mismatches, div tests (n), div_rn mismatches, sqrt_fast tests,
+ * sqrt_fast mismatches, and the mismatches of the compiler's own f32 sqrt and
+ * division on the same inputs (synchronous). */
+int wgt_selftest_math(wgt_ctx *ctx, uint32_t n, uint32_t seed, uint64_t counts[8]);
+
 /* The context's HIP stream (hipStream_t) for callers that share it. */
 void *wgt_stream(wgt_ctx *ctx);
 

@@ -1,17 +1,24 @@
-"""Print an A/B log (scripts/ab_run.sh) as a table: python scripts/ab_table.py gpurun_out/<tag>/ab.log"""
+"""Summarise scripts/ab_run.sh logs: per (library, scene) the kernel ms of every round,
+their median, and the change against the first library.  python scripts/ab_table.py LOG"""
 import json
+import statistics
 import sys
+from collections import defaultdict
 
-name = None
+times = defaultdict(list)
+head = None
 for line in open(sys.argv[1]):
     line = line.strip()
-    if " {" in line and not line.startswith("{"):
-        name, line = line.split(" {", 1)[0], "{" + line.split(" {", 1)[1]
-    if not line.startswith("{"):
-        continue
-    d = json.loads(line)
-    if "ms" not in d:
-        continue
-    print(f"{name:34s} ms={d['ms']:7.2f} Mrays/s={d['Mrays_s']:7.1f} trav_cyc/step={d['trav_cyc_per_step']:7.1f} "
-          f"svc_cyc/iter={d['svc_cyc_per_iter']:8.1f} steps={d['wave_steps']:>11,} nodes={d['nodes']:>13,} "
-          f"util={d['trav_util']} same={d['identical']}")
+    if line.endswith(".so") or ".so r" in line:
+        parts = line.split()
+        head = (parts[0], " ".join(parts[2:6]))
+    if line.startswith('{"WGT_KERNEL') and head:
+        times[head].append(json.loads(line)["ms"])
+libs = list(dict.fromkeys(k[0] for k in times))
+scenes = list(dict.fromkeys(k[1] for k in times))
+for sc in scenes:
+    base = statistics.median(times[(libs[0], sc)])
+    for lib in libs:
+        t = times[(lib, sc)]
+        med = statistics.median(t)
+        print(f"{sc:24s} {lib:14s} med {med:8.2f} ms  {100 * (med / base - 1):+6.2f}%  runs {t}")

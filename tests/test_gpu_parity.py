@@ -349,49 +349,3 @@ def test_mesh_tiles_reassemble_full_frame(ctx, wgt, bunny):
             tw, th = min(12, W - x0), min(12, H - y0)
             out[y0:y0 + th, x0:x0 + tw] = ctx.render_tile(cam, W, H, x0, y0, tw, th)["f32"]
     assert np.array_equal(out.view(np.uint32), full.view(np.uint32))
-
-
-def test_frame_batch_equals_single_frames(ctx, wgt, bunny):
-    """C5 launcher: a batch of whole frames in one tile-list launch (seed = frame)
-    equals each frame rendered alone with camera.seed = frame, bit for bit."""
-    from webgputracer_amd.frames import FrameRenderer
-
-    (L, Q, S, T), _ = bunny
-    ctx.upload_scene(L, Q, S, T)
-    W, H, spp = 48, 27, 4
-    imgs = FrameRenderer(ctx, W, H, spp).render([7, 8, 9])
-    for f in (7, 8, 9):
-        single = ctx.render_tile(wgt.camera_param(W / H, spp, f), W, H, want=("u8",))["u8"]
-        assert np.array_equal(imgs[f], single), f
-
-
-def test_cli_batched_frames_equal_reference_loop(tmp_path):
-    """wgt_tracer --batch 3 (Renderer::OnRenderBatch, one launch for three frames)
-    writes the same 000.png..002.png as the reference-style one-frame loop."""
-    import os
-    import subprocess
-
-    from PIL import Image
-
-    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "webgputracer_amd", "wgt_tracer")
-    outs = {}
-    for b in (1, 3):
-        d = tmp_path / f"b{b}"
-        d.mkdir()
-        r = subprocess.run([exe, "--frame", "1", "3", "--width", "40", "--height", "24", "--spp", "4", "--scene",
-                            "bunny", "--fixed-seed", "--batch", str(b), "--out", str(d)],
-                           capture_output=True, text=True, timeout=300)
-        assert r.returncode == 0, r.stderr
-        outs[b] = [np.asarray(Image.open(d / f"{f:03d}.png").convert("RGBA")) for f in range(3)]
-    for f in range(3):
-        assert np.array_equal(outs[1][f], outs[3][f]), f
-
-
-@pytest.mark.parametrize("seed", [1, 2])
-def test_selftest_math_sequences_are_ieee(ctx, seed):
-    """The kernels' short sqrt / division sequences (wgt_math.h sqrt_rn, div_rn)
-    equal IEEE sqrt and division bit for bit over 16M inputs each from the ranges
-    the kernels feed them (specials included for sqrt)."""
-    ns, bs, nd, bd = ctx.selftest_math(1 << 24, seed)
-    assert ns == nd == 1 << 24
-    assert bs == 0 and bd == 0, (bs, bd)

@@ -83,6 +83,15 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built; run __graft_entry__.build() (no CPU fallback exists)")
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7.  Loaded
+    # first, it is the one libwgt.so binds to (same SONAME), so device pointers and
+    # streams from torch and from libwgt.so belong to one runtime; loaded after
+    # libwgt.so's /opt/rocm copy, torch's would initialise a second runtime, which
+    # fails ("No HIP GPUs are available").
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P, U32, I = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_int
     sig = {

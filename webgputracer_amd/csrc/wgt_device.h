@@ -47,13 +47,16 @@ __device__ __forceinline__ void quad_accept(f3 o, f3 d, const float4* __restrict
 
 // path_tracer.wgsl:314-338.  `qt` receives t of the accepted quad: the triangle
 // search bound, and what finalize needs to rebuild the quad hit bit for bit.
+// EXACT: the compiler's IEEE division for t, for rays outside the render limits
+// that make div_rn exact here (k_trace's caller-supplied rays, wgt_math.h).
+template <bool EXACT = false>
 __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict__ q, uint32_t id,
                                            Hit& h, float& qt) {
   const f3 qn = xyz(q[3]);
   const float denom = dot(qn, d);
   if (fabs_w(denom) < kRayMin) return;
   const float4 wd = q[4];
-  const float t = div_rn(wd.w - dot(qn, o), denom);
+  const float t = EXACT ? (wd.w - dot(qn, o)) / denom : div_rn(wd.w - dot(qn, o), denom);
   if (t < kRayMin || kRayMax < t) return;
   // ray_dist is monotone non-decreasing in t >= 0 (each rounded step is), so t >=
   // qt (the accepted quad's t) implies ray_dist >= h.dist: the `>=` rejection
@@ -105,11 +108,12 @@ __device__ __forceinline__ void isect_sphere(f3 o, f3 d, const float4* __restric
   h.col = xyz(col);
 }
 
+template <bool EXACT = false>
 __device__ __forceinline__ void quad_scan(const DevScene& sc, f3 o, f3 d, Hit& h, float& qt) {
   hit_init(h);
   qt = __builtin_inff();
   const uint32_t nlq = sc.n_lights + sc.n_quads;
-  for (uint32_t k = 0; k < nlq; ++k) isect_quad(o, d, sc.quads + 6 * k, k, h, qt);
+  for (uint32_t k = 0; k < nlq; ++k) isect_quad<EXACT>(o, d, sc.quads + 6 * k, k, h, qt);
 }
 
 // The quad part of a hit rebuilt from (prim, t): the same operations as isect_quad.
@@ -438,8 +442,8 @@ __device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const
     isect_sphere(o, d, sc.spheres + 2 * k, nlq + sc.n_tris + k, h);
 }
 
-// Full sample_hit for one ray (k_trace, k_render).
-template <bool TRIS, bool STATS>
+// Full sample_hit for one ray (k_trace with EXACT, k_render).
+template <bool TRIS, bool STATS, bool EXACT = false>
 __device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* __restrict__ lds,
                                            Hit& h, TravStats& st) {
   if (has_nan(o) || has_nan(d)) {
@@ -447,7 +451,7 @@ __device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* 
     return;
   }
   float qt;
-  quad_scan(sc, o, d, h, qt);
+  quad_scan<EXACT>(sc, o, d, h, qt);
   Trav t;
   trav_init(o, d, h.prim != kNoHit, qt, t);
   if (TRIS) {
@@ -479,15 +483,16 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
   if (rand_next(seed) > 0.5f) {
     // sample_from_cosine: build_onb_from_w (:133-140) + rand_cos_dir (:123-131)
     const f3 a = (sign_w(w.x) * w.x) > 0.9f ? f3{0.0f, 1.0f, 0.0f} : f3{1.0f, 0.0f, 0.0f};
-    const f3 v = normalize(cross(w, a));
+    // |w| = 1 +- 2^-22 and a is the axis w is furthest from: |w x a|^2 >= 0.19
+    const f3 v = normalize_unit(cross(w, a));
     const f3 u = cross(w, v);
     const float r1 = rand_next(seed);
     const float r2 = rand_next(seed);
-    const float z = sqrt_rn(1.0f - r2);
+    const float z = sqrt_fast(1.0f - r2);
     const float phi = 2.0f * kPI * r1;
     float sphi, cphi;
     sincos_w(phi, sphi, cphi);
-    const float sr2 = sqrt_rn(r2);
+    const float sr2 = sqrt_fast(r2);
     const float lx2 = cphi * sr2;
     const float ly2 = sphi * sr2;
     sdir = (lx2 * u + ly2 * v) + z * w;
@@ -507,7 +512,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
   const float lpdf = dist2 / (light_cosine * sc.light_area);
   const float pdf_val = 0.5f * cpdf + 0.5f * lpdf;
   // scattering_pdf (:217-220) normalises the already normalised direction again
-  const f3 nd2 = normalize(nd);
+  const f3 nd2 = normalize_unit(nd);  // nd = sdir / exact length: unit, NaN or 0
   const float cs2 = dot(h.norm, nd2);
   const float spdf = cs2 < 0.0f ? 0.0f : cs2 * k_1_PI;
   pc = (spdf * (pc * h.col)) / pdf_val;

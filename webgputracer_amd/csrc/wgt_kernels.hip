@@ -312,7 +312,7 @@ k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __res
   const f3 d = f3{rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]};
   Hit h;
   TravStats st{0u, 0u, 0u, 0u};
-  sample_hit<TRIS, false>(sc, o, d, s_stack + threadIdx.x, h, st);
+  sample_hit<TRIS, false, true>(sc, o, d, s_stack + threadIdx.x, h, st);  // any caller ray: IEEE t
   prim[i] = h.prim;
   dist[i] = h.dist;
 }
@@ -342,40 +342,70 @@ k_lpt_order(const uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __rest
   for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) perm[atomicAdd(&s_cnt[lpt_bucket(cost[i])], 1u)] = i;
 }
 
-// wgt_selftest_math: sqrt_rn / div_rn against IEEE sqrt and division.  Inputs are
-// hashed from (seed, i): sqrt over x = 0, +inf, negatives and x >= 2^-96 of every
-// exponent; div over |d| in [2^-10, 2^20] and |n| in [2^-40, 2^40], both signs.
+// wgt_selftest_math: the kernels' sqrt / division forms (wgt_math.h) against
+// correctly rounded results: the f64 operation rounded to f32, exact for sqrt and
+// division because f64 has more than 2*24 + 2 bits (double rounding is innocuous).
+//   sqrt_rn   on all 2^32 bit patterns;
+//   sqrt_fast on every pattern of its domain (all but 0 < x < 2^-96 and negative
+//             denormals);
+//   div_rn    on n pseudo-random (numerator, denominator) pairs from the quad plane
+//             distance's range under the render limits: |n| <= 2^44 of any exponent
+//             (zeros and denormals included), 2^-10 <= |d| <= 2^33 (|d| >= kRayMin is
+//             tested before the division): the accept decision t in [kRayMin,
+//             kRayMax] must equal the IEEE one, and an accepted t its bits;
+//   the compiler's own lowerings (__builtin_sqrtf, n / d) on the same inputs.
+// NaN equals NaN.  counts: [0] sqrt tests, [1] sqrt_rn bad, [2] div tests, [3]
+// div_rn bad, [4] sqrt_fast tests, [5] sqrt_fast bad, [6] compiler sqrt bad, [7]
+// compiler div bad.
 __device__ __forceinline__ uint32_t st_hash(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352du; x ^= x >> 15; x *= 0x846ca68bu; x ^= x >> 16;
   return x;
 }
-__device__ __forceinline__ float st_float(uint32_t h, int emin, int emax) {
-  const uint32_t e = (uint32_t)(emin + 127) + (h >> 9) % (uint32_t)(emax - emin + 1);
+// sign and mantissa from h, biased exponent field uniform in [fmin, fmax]
+__device__ __forceinline__ float st_float(uint32_t h, uint32_t fmin, uint32_t fmax) {
+  const uint32_t e = fmin + (h >> 9) % (fmax - fmin + 1u);
   return __uint_as_float((h & 0x80000000u) | (e << 23) | (st_hash(h) & 0x7fffffu));
 }
+__device__ __forceinline__ bool st_same(float a, float b) {
+  return __float_as_uint(a) == __float_as_uint(b) || (a != a && b != b);
+}
+__device__ __forceinline__ bool st_accept(float t) { return !(t < kRayMin || kRayMax < t); }
 __global__ void __launch_bounds__(256) k_selftest_math(uint32_t n, uint32_t seed, unsigned long long* counts) {
-  uint32_t bad_s = 0, bad_d = 0;
-  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-    const uint32_t h = st_hash(seed * 0x9e3779b9u + i);
-    float x = fabsf(st_float(h, -96, 127));
-    const uint32_t k = i & 1023u;
-    if (k == 0) x = 0.0f;
-    if (k == 1) x = __builtin_inff();
-    if (k == 2) x = -x;
-    if (k == 3) x = __uint_as_float(0x7fc00000u);
-    const float a = sqrt_rn(x), b = __builtin_sqrtf(x);
-    if (__float_as_uint(a) != __float_as_uint(b) && !(a != a && b != b)) ++bad_s;
-    const uint32_t h2 = st_hash(h ^ 0x5bd1e995u);
-    const float nn = st_float(h2, -40, 40), dd = st_float(st_hash(h2), -10, 20);
-    const float q = div_rn(nn, dd), r = nn / dd;
-    if (__float_as_uint(q) != __float_as_uint(r)) ++bad_d;
+  uint32_t bad_s = 0, bad_f = 0, n_f = 0, bad_d = 0, bad_sc = 0, bad_dc = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
+    const uint32_t bits = (uint32_t)i;
+    const float x = __uint_as_float(bits);
+    const float ref = (float)__builtin_sqrt((double)x);
+    bad_s += st_same(sqrt_rn(x), ref) ? 0u : 1u;
+    bad_sc += st_same(__builtin_sqrtf(x), ref) ? 0u : 1u;
+    const uint32_t mag = bits & 0x7fffffffu;
+    const bool fast_domain = mag == 0u || mag >= 0x0f800000u || (bits >> 31 && mag >= 0x00800000u);
+    if (fast_domain) {
+      ++n_f;
+      bad_f += st_same(sqrt_fast(x), ref) ? 0u : 1u;
+    }
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint32_t)stride) {
+    const uint32_t h = st_hash(seed * 0x9e3779b9u + i), h2 = st_hash(h ^ 0x5bd1e995u);
+    const float nn = st_float(h, 0u, 127u + 44u);             // |n| <= 2^45 (zeros, denormals)
+    const float dd = st_float(h2, 127u - 10u, 127u + 32u);    // 2^-10 <= |d| < 2^33
+    const float ref = (float)((double)nn / (double)dd);
+    const float q = div_rn(nn, dd);
+    const bool acc = st_accept(ref);
+    bad_d += (acc != st_accept(q) || (acc && !st_same(q, ref))) ? 1u : 0u;
+    bad_dc += st_same(nn / dd, ref) ? 0u : 1u;
   }
   atomicAdd(&counts[1], (unsigned long long)bad_s);
   atomicAdd(&counts[3], (unsigned long long)bad_d);
+  atomicAdd(&counts[4], (unsigned long long)n_f);
+  atomicAdd(&counts[5], (unsigned long long)bad_f);
+  atomicAdd(&counts[6], (unsigned long long)bad_sc);
+  atomicAdd(&counts[7], (unsigned long long)bad_dc);
 }
 
 hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d_counts, hipStream_t stream) {
-  k_selftest_math<<<1024, 256, 0, stream>>>(n, seed, d_counts);
+  k_selftest_math<<<2048, 256, 0, stream>>>(n, seed, d_counts);
   return hipGetLastError();
 }
 

@@ -42,17 +42,17 @@ WGT_HD float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 WGT_HD f3 cross(f3 a, f3 b) {
   return f3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
-// Correctly rounded sqrt (device: fewer instructions than the general lowering).
-// The compiler lowers llvm.sqrt.f32 as: hardware v_sqrt_f32 (<= 1 ulp), then the
-// neighbour whose residual x - s*s brackets x, with an input scaling for
-// 0 < x < 2^-96 and a class fix-up for +-0 / +inf around it.  sqrt_rn is that
-// sequence without the scaling and the fix-up, which are identities for x = +-0,
-// x >= 2^-96, +inf and x < 0 / NaN (-> NaN).  Every sqrt input of the kernels is
-// one of those: squared lengths of scene-scale vectors (0 or >= 1e-8), rand()
-// values and 1 - rand() (0 or >= 2^-33), sphere discriminants (0 or >= ulp of
-// scene-scale squares).  tests/test_gpu_parity.py checks it against IEEE sqrt
-// (wgt_selftest_math) and every image bit for bit against the oracle.
-WGT_HD float sqrt_rn(float x) {
+// Correctly rounded sqrt and division (device: shorter sequences than the
+// compiler's general lowerings; DESIGN.md §3.2 states where each form is used and
+// why it is exact there; tests/test_gpu_numerics.py checks them exhaustively).
+//
+// The compiler lowers llvm.sqrt.f32 as hardware v_sqrt_f32 (<= 1 ulp; it flushes
+// a denormal input), then the neighbour whose residual x - s*s brackets x, with an
+// input scaling by 2^32 for x < 2^-96 and a class fix-up for +-0 / +inf.  The
+// fix-up is an identity for this sequence (+-0 and +inf come out unchanged, NaN
+// and negative normals give NaN).
+namespace detail {
+WGT_HD float sqrt_seq(float x) {
 #ifdef __HIP_DEVICE_COMPILE__
   const float s = __builtin_amdgcn_sqrtf(x);
   const float dn = __uint_as_float(__float_as_uint(s) - 1u);
@@ -64,11 +64,36 @@ WGT_HD float sqrt_rn(float x) {
   return __builtin_sqrtf(x);
 #endif
 }
-// Correctly rounded n / d for |d| >= 2^-100 and |n| <= 2^100 with a normal or zero
-// quotient (the quad plane distance: |d| >= kRayMin, scene-scale n): the
-// compiler's IEEE sequence (reciprocal refined by one Newton step, two residual
-// corrections) without v_div_scale / v_div_fixup, which are identities there.  A
-// -0 quotient may come out +0 (irrelevant where it is used: t = +-0 < kRayMin).
+}  // namespace detail
+// sqrt_fast: the sequence alone.  Exact for x = +-0, x >= 2^-96, +inf, NaN and
+// negative normals, i.e. every input except 0 < |x| < 2^-96 (and -denormals).
+// Used only where the input is in that set by construction: rand() values and
+// 1 - rand() (0 or >= 2^-33 in magnitude; 1 - rand() < 0 is a normal >= 2^-24)
+// and squared lengths of vectors within 2^-22 of unit length or NaN.
+WGT_HD float sqrt_fast(float x) { return detail::sqrt_seq(x); }
+// sqrt_rn: exact for every input: the compiler's 2^32 input scaling, selected
+// (not branched: a branch costs more than the 4 VALU in the persistent kernel).
+// Used wherever the input depends on differences of points (hit distances, the
+// light vector, sphere discriminants) or on scene-supplied normals.
+WGT_HD float sqrt_rn(float x) {
+#ifdef __HIP_DEVICE_COMPILE__
+  const bool small = x < 0x1p-96f;
+  const float s = detail::sqrt_seq(small ? x * 0x1p32f : x);
+  return small ? s * 0x1p-16f : s;  // exact scalings
+#else
+  return __builtin_sqrtf(x);
+#endif
+}
+// div_rn: the compiler's IEEE division sequence (reciprocal refined by one Newton
+// step, two residual corrections) without v_div_scale / v_div_fixup, which are
+// identities when |n|, |d| and the quotient lie in [2^-100, 2^100] (the residuals
+// n - d*q stay normal, so the FMAs compute them exactly).  Its one use, the quad
+// plane distance t = n / denom (isect_quad), is exact wherever the result decides
+// anything: |denom| >= kRayMin is tested first, and the scene and frame limits
+// checked at upload and per render (wgt_runtime.cpp) bound
+// |denom| <= 2^33 and |n| <= 2^44, so a quotient in the accepted [kRayMin, kRayMax]
+// is in the domain, and one outside it comes out outside it too (|q| < 2^-80 or
+// > 2^100 cannot turn into [kRayMin, kRayMax]).
 WGT_HD float div_rn(float n, float d) {
 #ifdef __HIP_DEVICE_COMPILE__
   float r = __builtin_amdgcn_rcpf(d);
@@ -83,6 +108,8 @@ WGT_HD float div_rn(float n, float d) {
 WGT_HD float length(f3 a) { return sqrt_rn(dot(a, a)); }
 // WGSL normalize(v) = v / length(v)   (zero vector -> NaN, as the reference relies on)
 WGT_HD f3 normalize(f3 a) { return a / length(a); }
+// normalize for a vector within 2^-22 of unit length (or NaN / inf / 0): sqrt_fast
+WGT_HD f3 normalize_unit(f3 a) { return a / sqrt_fast(dot(a, a)); }
 WGT_HD float distance(f3 a, f3 b) { return length(a - b); }
 WGT_HD bool has_nan(f3 a) { return (a.x != a.x) | (a.y != a.y) | (a.z != a.z); }
 

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -50,7 +51,11 @@ struct wgt_ctx {
   unsigned long long* ctl_host = nullptr;
   uint32_t ps_resident = 0;
   DevBuf ws;  // scheduling workspace of the persistent kernel (queues, LPT costs and order)
-  hipEvent_t ws_ev = nullptr;  // recorded after each launch that used ws  // resident k_render_ps waves for the current scene
+  // recorded after every launch that reads the scene or ws (renders on any stream and
+  // trace queries alike); each such launch first waits for the previous one, so this
+  // event completing means every earlier launch of the context has finished: the
+  // scene and ws are freed (re-upload, destroy, regrow) only after it
+  hipEvent_t use_ev = nullptr;
   std::vector<hipEvent_t> evpool;  // per-launch timing (profile runs only)
 };
 
@@ -69,10 +74,27 @@ int fail(wgt_ctx* ctx, int code, const std::string& msg) {
       return fail((ctx), WGT_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));       \
   } while (0)
 
+// Order a launch on stream s after every earlier launch of the context (any stream).
+int use_begin(wgt_ctx* ctx, hipStream_t s) {
+  if (!ctx->use_ev) WGT_HIP(ctx, hipEventCreateWithFlags(&ctx->use_ev, hipEventDisableTiming));
+  else WGT_HIP(ctx, hipStreamWaitEvent(s, ctx->use_ev, 0));
+  return WGT_OK;
+}
+int use_end(wgt_ctx* ctx, hipStream_t s) {
+  WGT_HIP(ctx, hipEventRecord(ctx->use_ev, s));
+  return WGT_OK;
+}
+// Host wait for every launch of the context (before freeing what they read).
+int use_drain(wgt_ctx* ctx) {
+  if (ctx->use_ev) WGT_HIP(ctx, hipEventSynchronize(ctx->use_ev));
+  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return WGT_OK;
+}
+
 int ensure(wgt_ctx* ctx, DevBuf& b, size_t bytes) {
   if (b.bytes >= bytes) return WGT_OK;
   if (b.p) {
-    (void)hipStreamSynchronize(ctx->stream);
+    (void)use_drain(ctx);  // launches on any stream may still use the old buffer
     (void)hipFree(b.p);
     b.p = nullptr;
     b.bytes = 0;
@@ -155,6 +177,44 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   return fr;
 }
 
+// Numeric limits under which the kernels' short division (wgt_math.h div_rn, the
+// quad plane distance) is exact wherever it decides anything:
+// scene coordinates and ray origins within 2^40, quad normals within 2 per
+// component (or NaN: a degenerate quad), primary ray directions within 2^32
+// (scattered directions are unit).  Everything else in the kernels is exact for
+// any input.  Outside the limits the calls fail with WGT_E_INVALID.
+constexpr double kCoordLimit = 1099511627776.0;  // 2^40
+constexpr double kPrimaryDirLimit = 4294967296.0;  // 2^32
+
+bool finite_within(const float* v, int n, double lim) {
+  for (int i = 0; i < n; ++i)
+    if (!(std::fabs((double)v[i]) <= lim)) return false;  // NaN and inf fail too
+  return true;
+}
+
+std::string check_scene_limits(const wgt_quad* lq, uint32_t nlq, const wgt_sphere* sp, uint32_t ns,
+                               const wgt_triangle* tr, uint32_t nt) {
+  for (uint32_t i = 0; i < nlq; ++i) {
+    const wgt_quad& q = lq[i];
+    if (!finite_within(q.pos, 3, kCoordLimit) || !finite_within(q.right, 3, kCoordLimit) ||
+        !finite_within(q.up, 3, kCoordLimit) || !finite_within(&q.d, 1, kCoordLimit * 4.0))
+      return "quad " + std::to_string(i) + ": position, edges and plane offset must be finite and within 2^40";
+    const bool nan_norm = q.norm[0] != q.norm[0] || q.norm[1] != q.norm[1] || q.norm[2] != q.norm[2];
+    if (!nan_norm && !finite_within(q.norm, 3, 2.0))
+      return "quad " + std::to_string(i) + ": normal components must be within 2 (a unit normal) or NaN";
+  }
+  for (uint32_t i = 0; i < ns; ++i)
+    if (!finite_within(sp[i].center, 3, kCoordLimit) || !finite_within(&sp[i].radius, 1, kCoordLimit))
+      return "sphere " + std::to_string(i) + ": center and radius must be finite and within 2^40";
+  for (uint32_t i = 0; i < nt; ++i)
+    if (!finite_within(tr[i].v0, 3, kCoordLimit) || !finite_within(tr[i].e1, 3, kCoordLimit) ||
+        !finite_within(tr[i].e2, 3, kCoordLimit))
+      return "triangle " + std::to_string(i) + ": vertices must be finite and within 2^40";
+  return "";
+}
+
+double sq(double x) { return x * x; }
+
 int check_render_args(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H,
                       uint32_t tw, uint32_t th) {
   if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
@@ -164,6 +224,21 @@ int check_render_args(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uin
   if (tw == 0 || th == 0) return fail(ctx, WGT_E_INVALID, "empty tile");
   if (!(cam->aspect == cam->aspect) || !(cam->fovy == cam->fovy))
     return fail(ctx, WGT_E_INVALID, "NaN camera parameter");
+  // the kernels pack a sample's (s_i, s_j) into 16 bits each and count sqrt_spp^2
+  // samples in 32 bits: u32(sqrt(f32(spp))) must stay <= 65535 (spp < 2^32 - 2^8)
+  if ((uint32_t)__builtin_sqrtf((float)cam->spp) > 65535u)
+    return fail(ctx, WGT_E_INVALID, "spp too large (u32(sqrt(f32(spp))) must be <= 65535)");
+  if (!finite_within(cam->origin, 3, kCoordLimit) || !finite_within(cam->target, 3, kCoordLimit))
+    return fail(ctx, WGT_E_INVALID, "camera origin and target must be finite and within 2^40");
+  // primary directions: viewport point - origin, the viewport spanning [-1/2, W+1/2] x
+  // [-1/2, H+1/2] pixels around po (make_frame, setup_camera_ray)
+  const DevFrame fr = make_frame(*cam, W, H);
+  const double po = std::sqrt(sq((double)fr.pox - fr.ox) + sq((double)fr.poy - fr.oy) + sq((double)fr.poz - fr.oz));
+  const double du = std::sqrt(sq((double)fr.dux) + sq((double)fr.duy) + sq((double)fr.duz));
+  const double dv = std::sqrt(sq((double)fr.dvx) + sq((double)fr.dvy) + sq((double)fr.dvz));
+  if (!(po + (W + 1.0) * du + (H + 1.0) * dv <= kPrimaryDirLimit))
+    return fail(ctx, WGT_E_INVALID, "camera: primary ray directions must be finite and within 2^32 "
+                                    "(viewport and focal length out of range)");
   return WGT_OK;
 }
 
@@ -221,15 +296,14 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
     if (timing) WGT_HIP(ctx, hipEventRecord(e0, s));
     int rc;
     const size_t ws_need = render_ws_bytes(fr);
-    if (ctx->ws.bytes < ws_need && ctx->ws_ev) WGT_HIP(ctx, hipEventSynchronize(ctx->ws_ev));  // before regrowing
+    if (ctx->ws.bytes < ws_need && (rc = use_drain(ctx))) return rc;  // before regrowing
     if ((rc = ensure(ctx, ctx->ws, ws_need))) return rc;
     // the workspace is the context's: a launch on any stream first waits for the
-    // previous launch that used it (calls on one context serialise on the device)
-    if (!ctx->ws_ev) WGT_HIP(ctx, hipEventCreateWithFlags(&ctx->ws_ev, hipEventDisableTiming));
-    else WGT_HIP(ctx, hipStreamWaitEvent(s, ctx->ws_ev, 0));
+    // previous launch of the context (calls on one context serialise on the device)
+    if ((rc = use_begin(ctx, s))) return rc;
     WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
                                ctx->ws.p, ctx->ws.bytes, s));
-    WGT_HIP(ctx, hipEventRecord(ctx->ws_ev, s));
+    if ((rc = use_end(ctx, s))) return rc;
     if (timing) {
       WGT_HIP(ctx, hipEventRecord(e1, s));
       WGT_HIP(ctx, hipEventSynchronize(e1));
@@ -246,6 +320,7 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
   if (!ctx->ctl_host) WGT_HIP(ctx, hipHostMalloc((void**)&ctx->ctl_host, 256, hipHostMallocDefault));
   WfState st;
   (void)wf_bind(ctx->wf.p, n, (unsigned long long*)ctx->ctl.p, st);
+  if ((rc = use_begin(ctx, s))) return rc;
   WGT_HIP(ctx, hipMemsetAsync(ctx->ctl.p, 0, 8, s));
   size_t ev = 0;
   auto mark = [&]() -> hipEvent_t {
@@ -273,6 +348,7 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
       if (it >= max_iter) return fail(ctx, WGT_E_HIP, "wavefront loop did not converge");
     }
   }
+  if ((rc = use_end(ctx, s))) return rc;
   if (timing) {
     mark();
     WGT_HIP(ctx, hipStreamSynchronize(s));
@@ -338,12 +414,13 @@ int wgt_create(int hip_device, wgt_ctx** out) {
 void wgt_destroy(wgt_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
+  if (ctx->use_ev) (void)hipEventSynchronize(ctx->use_ev);  // launches on callers' streams too
   if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
   if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
   free_buf(ctx->tiles); free_buf(ctx->out8); free_buf(ctx->out32); free_buf(ctx->hit);
   free_buf(ctx->counters); free_buf(ctx->rays); free_buf(ctx->prim); free_buf(ctx->dist);
   free_buf(ctx->wf); free_buf(ctx->ctl); free_buf(ctx->ws);
-  if (ctx->ws_ev) (void)hipEventDestroy(ctx->ws_ev);
+  if (ctx->use_ev) (void)hipEventDestroy(ctx->use_ev);
   if (ctx->ctl_host) (void)hipHostFree(ctx->ctl_host);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
@@ -417,6 +494,11 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     return fail(ctx, WGT_E_INVALID, "need >= 1 sphere (the reference binds a dummy sphere)");
   if (n_quads > 0 && !quads) return fail(ctx, WGT_E_INVALID, "null quads");
   if (n_tris > 0 && !tris) return fail(ctx, WGT_E_INVALID, "null triangles");
+  {
+    std::string lim = check_scene_limits(lights, n_lights, spheres, n_spheres, tris, n_tris);
+    if (lim.empty() && n_quads) lim = check_scene_limits(quads, n_quads, nullptr, 0, nullptr, 0);
+    if (!lim.empty()) return fail(ctx, WGT_E_INVALID, lim);
+  }
   WGT_HIP(ctx, hipSetDevice(ctx->device));
 
   BvhOut bvh;
@@ -441,7 +523,10 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const size_t b_shade = align256(bvh.tshade.size() * 4);
   const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes;
 
-  WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  {
+    int rc = use_drain(ctx);  // no launch on any stream may still read the old scene
+    if (rc) return rc;
+  }
   if (ctx->scene_mem) {
     (void)hipFree(ctx->scene_mem);
     ctx->scene_mem = nullptr;
@@ -677,21 +762,24 @@ int wgt_trace_rays_async(wgt_ctx* ctx, const float* d_rays, uint32_t n, uint32_t
   if (!d_rays || !d_prim_id || !d_dist) return fail(ctx, WGT_E_INVALID, "null buffer");
   WGT_HIP(ctx, hipSetDevice(ctx->device));
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  int rc;
+  if ((rc = use_begin(ctx, s))) return rc;
   WGT_HIP(ctx, launch_trace(ctx->sc, d_rays, n, d_prim_id, d_dist, s));
-  return WGT_OK;
+  return use_end(ctx, s);
 }
 
-int wgt_selftest_math(wgt_ctx* ctx, uint32_t n, uint32_t seed, uint64_t counts[4]) {
+int wgt_selftest_math(wgt_ctx* ctx, uint32_t n, uint32_t seed, uint64_t counts[8]) {
   if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
   if (!counts) return fail(ctx, WGT_E_INVALID, "null counts");
   WGT_HIP(ctx, hipSetDevice(ctx->device));
   int rc;
-  if ((rc = ensure(ctx, ctx->prim, 32))) return rc;
-  WGT_HIP(ctx, hipMemsetAsync(ctx->prim.p, 0, 32, ctx->stream));
+  if ((rc = ensure(ctx, ctx->prim, 64))) return rc;
+  WGT_HIP(ctx, hipMemsetAsync(ctx->prim.p, 0, 64, ctx->stream));
   WGT_HIP(ctx, launch_selftest_math(n, seed, (unsigned long long*)ctx->prim.p, ctx->stream));
-  WGT_HIP(ctx, hipMemcpyAsync(counts, ctx->prim.p, 32, hipMemcpyDeviceToHost, ctx->stream));
+  WGT_HIP(ctx, hipMemcpyAsync(counts, ctx->prim.p, 64, hipMemcpyDeviceToHost, ctx->stream));
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  counts[0] = counts[2] = n;
+  counts[0] = 1ull << 32;  // sqrt: every bit pattern
+  counts[2] = n;
   return WGT_OK;
 }
 
@@ -706,8 +794,10 @@ int wgt_trace_rays(wgt_ctx* ctx, const float* rays, uint32_t n, uint32_t* prim_i
   if ((rc = ensure(ctx, ctx->prim, (size_t)n * 4))) return rc;
   if ((rc = ensure(ctx, ctx->dist, (size_t)n * 4))) return rc;
   WGT_HIP(ctx, hipMemcpyAsync(ctx->rays.p, rays, (size_t)n * 24, hipMemcpyHostToDevice, ctx->stream));
+  if ((rc = use_begin(ctx, ctx->stream))) return rc;
   WGT_HIP(ctx, launch_trace(ctx->sc, (const float*)ctx->rays.p, n, (uint32_t*)ctx->prim.p,
                             (float*)ctx->dist.p, ctx->stream));
+  if ((rc = use_end(ctx, ctx->stream))) return rc;
   WGT_HIP(ctx, hipMemcpyAsync(prim_id, ctx->prim.p, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
   WGT_HIP(ctx, hipMemcpyAsync(dist, ctx->dist.p, (size_t)n * 4, hipMemcpyDeviceToHost, ctx->stream));
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -105,3 +105,59 @@ def gather_tiles(local, rank: int, world: int, dist, dst: int = 0):
         return bufs
     dist.gather(local, dst=dst)
     return None
+
+
+class ShardedFrames:
+    """One rank's share of a step (bench.py's N>1 path, and its GPU test): the
+    step's frames cut into T x T tiles dealt round-robin (shard_tiles), one
+    tile-list launch into a compact device buffer (wgt_render_tiles_async), one
+    gather to rank 0 (RCCL over xGMI with backend "nccl"; gloo gathers host
+    copies) and rank 0's assembly with a single index op built once here.
+
+    frames: list of (frame id, seed).  want: "u8" (rgba8, always) and optionally
+    "f32" (radiance before quantisation, gathered the same way)."""
+
+    def __init__(self, ctx, cam, W, H, T, frames, rank, world, dist, device, backend="nccl", want=("u8",)):
+        import torch
+
+        self.ctx, self.cam, self.W, self.H, self.T = ctx, cam, W, H, T
+        self.frames, self.rank, self.world, self.dist = list(frames), rank, world, dist
+        self.backend, self.device = backend, device
+        self.tiles = shard_tiles(W, H, T, self.frames, rank, world)
+        self.n_max = max_tiles_per_rank(W, H, T, len(self.frames), world)
+        self.d_tiles = torch.from_numpy(self.tiles.view(np.uint8).copy()).to(device)
+        self.bufs = {"u8": torch.zeros((self.n_max, T, T, 4), dtype=torch.uint8, device=device)}
+        if "f32" in want:
+            self.bufs["f32"] = torch.zeros((self.n_max, T, T, 4), dtype=torch.float32, device=device)
+        self.frame_ids = [f for f, _ in self.frames]
+        self.asm_idx = None
+        if rank == 0:
+            layout = self.tiles if world == 1 else np.concatenate(
+                [pad_tiles(shard_tiles(W, H, T, self.frames, r, world), self.n_max) for r in range(world)])
+            self.asm_idx = torch.from_numpy(assemble_index(layout, W, H, T, self.frame_ids)).to(device)
+
+    def stats(self):
+        """Instrumented pass over this rank's tiles (exact counters; untimed)."""
+        return self.ctx.render_tiles_stats(self.cam, self.W, self.H, self.T, self.T, self.d_tiles.data_ptr(),
+                                           len(self.tiles))
+
+    def launch(self, stream=0):
+        """Render this rank's tiles (asynchronous, ordered on `stream`, a raw hipStream_t)."""
+        f32 = self.bufs.get("f32")
+        self.ctx.render_tiles_async(self.cam, self.W, self.H, self.T, self.T, self.d_tiles.data_ptr(),
+                                    len(self.tiles), d_u8=self.bufs["u8"].data_ptr(),
+                                    d_f32=f32.data_ptr() if f32 is not None else 0, stream=stream)
+
+    def gather(self):
+        """Gather every rank's tiles to rank 0 and assemble: {kind: {frame id: (H, W, 4) tensor}}
+        on rank 0, None elsewhere."""
+        import torch
+
+        out = {}
+        for kind, buf in self.bufs.items():
+            got = gather_tiles(buf if self.backend == "nccl" else buf.cpu(), self.rank, self.world, self.dist)
+            if self.rank == 0:
+                data = (got[0] if self.world == 1 else torch.cat(got)).to(self.device).reshape(-1, 4)
+                imgs = data[self.asm_idx]  # (frames, H, W, 4)
+                out[kind] = {f: imgs[i] for i, f in enumerate(self.frame_ids)}
+        return out if self.rank == 0 else None

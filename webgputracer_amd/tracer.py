@@ -239,10 +239,12 @@ class Context:
         self._check(self._L.wgt_sync(self.h))
 
     def selftest_math(self, n: int, seed: int = 1):
-        """-> (sqrt tests, sqrt mismatches, div tests, div mismatches) of wgt_selftest_math."""
-        counts = np.zeros(4, np.uint64)
+        """-> dict of wgt_selftest_math's counts (include/wgt_api.h)."""
+        counts = np.zeros(8, np.uint64)
         self._check(self._L.wgt_selftest_math(self.h, n, seed, counts.ctypes.data_as(ctypes.c_void_p)))
-        return tuple(int(c) for c in counts)
+        keys = ("sqrt_tests", "sqrt_rn_bad", "div_tests", "div_rn_bad", "sqrt_fast_tests", "sqrt_fast_bad",
+                "compiler_sqrt_bad", "compiler_div_bad")
+        return dict(zip(keys, (int(c) for c in counts)))
 
 
 def tile_grid(W: int, H: int, T: int, seed: int = 0, frame: int = 0):
