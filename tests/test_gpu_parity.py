@@ -349,3 +349,17 @@ def test_mesh_tiles_reassemble_full_frame(ctx, wgt, bunny):
             tw, th = min(12, W - x0), min(12, H - y0)
             out[y0:y0 + th, x0:x0 + tw] = ctx.render_tile(cam, W, H, x0, y0, tw, th)["f32"]
     assert np.array_equal(out.view(np.uint32), full.view(np.uint32))
+
+
+def test_triangle_tie_rule_on_gpu(ctx, wgt, oracle):
+    """tests/test_oracle_kats.py::test_triangle_tie_rule_is_min_t_then_index through
+    the kernel: equal ray_dist, different t -> the smaller t (index 1) wins."""
+    from test_oracle_kats import TIE_D, TIE_O, tie_triangles
+
+    L, Q, S = wgt.cornell_scene()
+    T = tie_triangles(wgt)
+    ctx.upload_scene(L, Q[:0], S, T)
+    prim, dist = ctx.trace_rays(TIE_O, TIE_D)
+    rp, rd = oracle.OracleScene(L, Q[:0], S, T).trace(TIE_O, TIE_D)
+    assert prim[0] == rp[0] == len(L) + 1
+    assert dist.view(np.uint32)[0] == rd.view(np.uint32)[0]

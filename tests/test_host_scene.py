@@ -58,6 +58,24 @@ def test_obj_reader_fan_triangulation(wgt, oracle, tmp_path):
     assert tris.tobytes() == ref.tobytes()
 
 
+def test_obj_reader_nonplanar_quad_is_a_fan_from_vertex_0(wgt, oracle, tmp_path):
+    """Polygons are split as a fan from their first vertex, (0,1,2), (0,2,3), ...:
+    an assumption about tinyobjloader's default triangulation (its submodule is
+    empty in the reference, so the rule is unpinned).  On this
+    non-planar quad the shorter-diagonal rule some tinyobjloader versions use would
+    split along 1-3 instead, giving different triangles; switching rules must be a
+    visible choice."""
+    p = tmp_path / "q.obj"
+    p.write_text("v 0 0 0\nv 1 0 0\nv 1 1 1\nv 0 1 0\nf 1 2 3 4\n")
+    tris = wgt.load_obj(p)
+    verts = np.float32([[0, 0, 0], [1, 0, 0], [1, 1, 1], [0, 1, 0]])
+    white = np.float32([0.73, 0.73, 0.73])  # color_util.h:8, load_obj's default
+    fan = oracle.make_triangles(verts[[0, 0]], verts[[1, 2]], verts[[2, 3]], white)
+    assert tris.tobytes() == fan.tobytes()
+    shorter = oracle.make_triangles(verts[[0, 1]], verts[[1, 2]], verts[[3, 3]], white)
+    assert tris.tobytes() != shorter.tobytes()
+
+
 def test_obj_reader_errors(wgt, tmp_path):
     p = tmp_path / "bad.obj"
     p.write_text("v 0 0 0\nf 1 2 3\n")

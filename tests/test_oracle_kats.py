@@ -159,3 +159,34 @@ def test_oracle_bvh_equals_bruteforce(oracle, wgt):
     b = sc.trace_tris(o, d, brute=True)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32))
     assert np.mean(a[0] != oracle.NO_HIT) > 0.5
+
+
+# Two triangles whose hits round to the same ray_dist at different t (found by a
+# search with the oracle): A = tri index 0 at z = 0.5000009 (t = 5.351351), B = tri
+# index 1 at z = 0.500001 (t = 5.3513503), ray from (0.3, 0.3, 20.3) along -3.7 z.
+TIE_O = np.array([[0.3, 0.3, 20.3]], np.float32)
+TIE_D = np.array([[0.0, 0.0, -3.7]], np.float32)
+
+
+def tie_triangles(wgt):
+    z = [np.float32(0.5000009), np.float32(0.500001)]
+    return np.concatenate([wgt.make_triangles(np.array([[[-1, -1, zz], [3, -1, zz], [-1, 3, zz]]], np.float32))
+                           for zz in z])
+
+
+def test_triangle_tie_rule_is_min_t_then_index(oracle, wgt):
+    """The closest triangle is the minimum of (t, index), a
+    deliberate departure from the reference's sequential scan rule for quads and
+    spheres (`ray_dist >= closest.dist` rejects, path_tracer.wgsl:320-325), which
+    would keep the FIRST of two hits with equal rounded ray_dist.  Here the two
+    hits have the same ray_dist but B (index 1) has the smaller t, so B wins; a
+    future change to the rule fails this test."""
+    L, Q, S = wgt.cornell_scene()
+    A, B = tie_triangles(wgt)
+    dist = [oracle.OracleScene(L, Q[:0], S, T[None]).trace(TIE_O, TIE_D)[1][0] for T in (A, B)]
+    t = [oracle.OracleScene(L, Q[:0], S, T[None]).trace_tris(TIE_O, TIE_D)[1][0] for T in (A, B)]
+    assert dist[0] == dist[1] and t[1] < t[0]
+    osc = oracle.OracleScene(L, Q[:0], S, tie_triangles(wgt))
+    for brute in (True, False):
+        prim, d = osc.trace(TIE_O, TIE_D, brute=brute)
+        assert prim[0] == len(L) + 1 and d[0] == dist[1]  # triangle B, not the first-scanned A
