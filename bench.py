@@ -40,6 +40,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # 4th, the padded box, only for a candidate closest hit), a traced ray 32 B of
 # per-triangle shading data
 NODE_BYTES, CNODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 48, 32
+# SURVEY §8(d)'s format-independent figure: 32 B per BVH node visit, 48 B per triangle
+# test, 32 B of shading record per traced ray (the same at any node encoding)
+SURVEY_NODE_BYTES = 32
+L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the 8 XCDs
+L2_CALIB_JSON = os.path.join(ROOT, "profiles", "l2_calibration.json")
 
 
 def dominant_kernel(compact: bool, waves: int, tris: bool = True) -> str:
@@ -73,6 +78,8 @@ def parse():
                    help="nccl = RCCL over xGMI (default); gloo only to rehearse N ranks on fewer GPUs")
     p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                    help="weak: one frame per GPU per step (default); strong: one frame split over the GPUs")
+    p.add_argument("--stats-reps", type=int, default=2,
+                   help="instrumented counting passes (node/triangle counts vary slightly between schedules)")
     p.add_argument("--check", action="store_true",
                    help="rank 0 compares the assembled frames with single-launch renders (bit-exact)")
     return p.parse_args()
@@ -85,17 +92,38 @@ def build_scene(w, kind):
     return w.mesh_scene(kind)
 
 
+def baseline_threads():
+    """Threads for the CPU baseline: the CPUs this process may run on, capped by
+    OMP_NUM_THREADS where the launcher sets it (the GPU box sets it to the box's CPU
+    share, 16, and asks that worker pools stay within it)."""
+    n = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(n, omp) if omp > 0 else n), n
+
+
 def cpu_baseline(args, scene, rank, world):
-    """The oracle (CPU port, OpenMP) on a bounded row sample of the same workload."""
+    """The oracle (CPU port, OpenMP) on a bounded row sample of the same workload,
+    timed with its x86-64-v3 build (oracle/Makefile: liboracle_v3.so), which is first
+    checked bit for bit against the reference build liboracle.so on a small tile."""
     if rank != 0 or world != 1 or args.no_cpu_baseline:
         return None
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
 
     L, Q, S, T = scene
-    osc = po.OracleScene(L, Q, S, T)
-    cores = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    cores, affinity = baseline_threads()
     cam = po.camera_param(args.width / args.height, args.spp, 0)
+    check = {}
+    for build in ("liboracle.so", "liboracle_v3.so"):
+        po.use_build(build)
+        osc = po.OracleScene(L, Q, S, T)
+        check[build] = osc.render(po.camera_param(args.width / args.height, 4, 0), args.width, args.height,
+                                  args.width // 2, args.height // 2, 16, 8, nthreads=cores, want=("f32",))["f32"]
+        osc.close()
+    same = bool(np.array_equal(check["liboracle.so"].view(np.uint32), check["liboracle_v3.so"].view(np.uint32)))
+    po.use_build("liboracle_v3.so" if same else "liboracle.so")
+    osc = po.OracleScene(L, Q, S, T)
+
     def run(rows):
         # rows spread evenly over the frame, full width, same spp/seed as the GPU frame
         ys = np.linspace(0, args.height - 1, rows).astype(int)
@@ -112,8 +140,11 @@ def cpu_baseline(args, scene, rank, world):
         rows = int(min(args.height, max(2, 2 * 15.0 / max(dt, 1e-3))))
     traced, dt = run(rows)
     osc.close()
+    build = "liboracle_v3.so (x86-64-v3, bit-identical to liboracle.so on a check tile)" if same else \
+        "liboracle.so (the x86-64-v3 build differed on the check tile)"
     return {"value": traced / dt / 1e6, "unit": "Mrays/s", "cores": cores, "kind": "port",
-            "sample": f"oracle (oracle/wgt_oracle.c, OpenMP {cores} threads) on {rows} full-width rows "
+            "sample": f"oracle/wgt_oracle.c as {build}, OpenMP {cores} threads (affinity {affinity} CPUs, "
+                      f"OMP_NUM_THREADS {os.environ.get('OMP_NUM_THREADS', 'unset')}), on {rows} full-width rows "
                       f"of the same {args.width}x{args.height}/{args.spp}spp frame (seed 0): {traced} traced "
                       f"rays in {dt:.1f} s"}
 
@@ -156,8 +187,11 @@ def main():
     # the rank's tiles, its compact output buffer and (rank 0) the assembly index, all resident
     shard = wdist.ShardedFrames(ctx, cam, W, H, T, frames, rank, world, dist, dev, backend=args.dist_backend)
 
-    # instrumented pass (untimed): exact counts for this rank's tiles
-    st = shard.stats()
+    # instrumented passes (untimed): exact ray/sample counts for this rank's tiles.  The
+    # node / triangle counts depend slightly on the schedule (which lanes run the
+    # speculative second leaf of a step), so the spread over the passes is reported
+    sts = [shard.stats() for _ in range(max(args.stats_reps, 1))]
+    st = sts[0]
 
     # a real (non-NULL) stream: the launch, the events and the gather are ordered on it
     stream = torch.cuda.Stream(device=dev)
@@ -220,15 +254,27 @@ def main():
         node_b = CNODE_BYTES if compact else NODE_BYTES
         bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-        traffic = None
+        survey_bytes = mine[4] * SURVEY_NODE_BYTES + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES
+        traffic, l2 = None, None
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             tj = tj.get(f"{args.scene}-{W}x{H}-{spp}spp", {})  # one entry per workload
             if tj.get("n_gpus", 1) == 1 and world == 1 and tj.get("kernel") == kernel:
                 traffic = tj.get("hbm_bytes_per_launch")
-        except (OSError, ValueError):
+                req = tj.get("tcc_requests_per_launch")
+                with open(L2_CALIB_JSON) as f:
+                    bpr = json.load(f)["bytes_per_request"]
+                if req and kern_ms > 0:
+                    l2_gbs = req * bpr / (kern_ms * 1e-3) / 1e9
+                    l2 = {"requests_per_launch": req, "bytes_per_request": bpr, "achieved": round(l2_gbs, 1),
+                          "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": round(l2_gbs / L2_PEAK_GBS, 4),
+                          "hit_rate": tj.get("tcc_hit_rate"), "source": tj.get("source"),
+                          "calibration": os.path.relpath(L2_CALIB_JSON, ROOT)}
+        except (OSError, ValueError, KeyError):
             pass
+        nodes = [int(x["node_visits"]) for x in sts]
+        tris = [int(x["tri_tests"]) for x in sts]
         n_tris = info["n_tris"]
         line = {
             "metric": METRIC,
@@ -257,7 +303,21 @@ def main():
                            "bvh_nodes": "compact 64 B + 16 B refs" if compact else "128 B",
                            "bytes_per_unit": {"node": node_b, "tri": TRI_BYTES, "shade_per_ray": SHADE_BYTES}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic},
+                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                         # the same launch priced with SURVEY §8(d)'s encoding-independent bytes
+                         "survey_8d": {"bytes_per_launch": int(survey_bytes),
+                                       "achieved": round(survey_bytes / (kern_ms * 1e-3) / 1e9, 2) if kern_ms > 0
+                                       else 0.0,
+                                       "frac": round(survey_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                                       if kern_ms > 0 else 0.0,
+                                       "bytes_per_unit": {"node": SURVEY_NODE_BYTES, "tri": TRI_BYTES,
+                                                          "shade_per_ray": SHADE_BYTES}},
+                         # L2 request traffic of the timed kernel (PMC pass, calibrated request size)
+                         "l2": l2,
+                         # node/triangle counts come from instrumented passes of the same tiles, whose
+                         # schedule differs from the timed launch's: their spread over the passes
+                         "count_spread": {"passes": len(sts), "node_visits": [min(nodes), max(nodes)],
+                                          "tri_tests": [min(tris), max(tris)]}},
             "cpu_baseline": base,
         }
         if check is not None:

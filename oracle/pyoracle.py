@@ -38,6 +38,14 @@ def build() -> None:
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
 
+def use_build(name: str = "liboracle.so"):
+    """Select the oracle build to load (bench.py's cpu_baseline times liboracle_v3.so,
+    the same source built for x86-64-v3); resets the loaded library."""
+    global _lib, _LIB_PATH
+    _lib = None
+    _LIB_PATH = os.path.join(_HERE, "build", name)
+
+
 def lib():
     global _lib
     if _lib is None:
@@ -118,12 +126,13 @@ class OracleScene:
         tris = np.zeros(0, TRI_DTYPE) if tris is None else np.ascontiguousarray(tris)
         self._keep.append(tris)
         self.n_lights, self.n_quads, self.n_spheres, self.n_tris = len(lights), len(quads), len(spheres), len(tris)
-        self.h = lib().o_scene_create(_p(self._keep[0]), len(lights), _p(self._keep[1]), len(quads),
+        self._L = lib()  # the build this scene was created with (use_build may switch later)
+        self.h = self._L.o_scene_create(_p(self._keep[0]), len(lights), _p(self._keep[1]), len(quads),
                                       _p(self._keep[2]), len(spheres), _p(tris), len(tris))
 
     def close(self):
         if self.h:
-            lib().o_scene_destroy(self.h)
+            self._L.o_scene_destroy(self.h)
             self.h = None
 
     def __del__(self):
@@ -139,7 +148,7 @@ class OracleScene:
         u8 = np.zeros((th, tw, 4), np.uint8) if "u8" in want else None
         hit = np.zeros((th, tw), np.uint32) if "hit" in want else None
         cnt = np.zeros(8, np.uint64)
-        rc = lib().o_render(self.h, _p(cam), W, H, x0, y0, tw, th, _p(f32), _p(u8), _p(hit), _p(cnt),
+        rc = self._L.o_render(self.h, _p(cam), W, H, x0, y0, tw, th, _p(f32), _p(u8), _p(hit), _p(cnt),
                             nthreads)
         if rc != 0:
             raise RuntimeError(f"o_render failed: {rc}")
@@ -151,7 +160,7 @@ class OracleScene:
         n = len(start)
         pid = np.zeros(n, np.uint32)
         dist = np.zeros(n, np.float32)
-        lib().o_trace(self.h, n, _p(start), _p(direction), _p(pid), _p(dist), int(brute))
+        self._L.o_trace(self.h, n, _p(start), _p(direction), _p(pid), _p(dist), int(brute))
         return pid, dist
 
     def trace_tris(self, start, direction, brute=False):
@@ -160,5 +169,5 @@ class OracleScene:
         n = len(start)
         tid = np.zeros(n, np.uint32)
         t = np.zeros(n, np.float32)
-        lib().o_trace_tris(self.h, n, _p(start), _p(direction), _p(tid), _p(t), int(brute))
+        self._L.o_trace_tris(self.h, n, _p(start), _p(direction), _p(tid), _p(t), int(brute))
         return tid, t

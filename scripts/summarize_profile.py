@@ -86,6 +86,9 @@ def main():
         wl = line["config"]["workload"]
         table[wl] = {"workload": wl, "n_gpus": 1, "kernel": timed, "hbm_bytes_per_launch": hbm,
                      "fetch_size_kib": fetch, "write_size_kib": write, "source": f"profiles/{rnd}_{tag}_summary.md"}
+        if hit + miss > 0:  # L2 requests of the timed kernel (bench.py's roofline.l2)
+            table[wl]["tcc_requests_per_launch"] = hit + miss
+            table[wl]["tcc_hit_rate"] = round(hit / (hit + miss), 4)
         json.dump(table, open(tpath, "w"), indent=1)
     sq = {c: per.get((timed, c)) for c in ("SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")}
     if all(v for v in sq.values()):
