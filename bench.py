@@ -80,6 +80,9 @@ def parse():
                    help="weak: one frame per GPU per step (default); strong: one frame split over the GPUs")
     p.add_argument("--stats-reps", type=int, default=2,
                    help="instrumented counting passes (node/triangle counts vary slightly between schedules)")
+    p.add_argument("--pipeline", type=int, default=2,
+                   help="frames in flight: step k runs on the context's pipeline stream k %% P, so the next "
+                        "frame fills the CUs the previous frame's end-of-launch drain leaves idle (1 = serial)")
     p.add_argument("--check", action="store_true",
                    help="rank 0 compares the assembled frames with single-launch renders (bit-exact)")
     return p.parse_args()
@@ -185,7 +188,9 @@ def main():
     dev = torch.device("cuda", local)
     cam = w.camera_param(W / H, spp, 0)  # per-tile seeds override cam.seed
     # the rank's tiles, its compact output buffer and (rank 0) the assembly index, all resident
-    shard = wdist.ShardedFrames(ctx, cam, W, H, T, frames, rank, world, dist, dev, backend=args.dist_backend)
+    P = max(1, min(args.pipeline, 4))
+    shard = wdist.ShardedFrames(ctx, cam, W, H, T, frames, rank, world, dist, dev, backend=args.dist_backend,
+                                depth=P)
 
     # instrumented passes (untimed): exact ray/sample counts for this rank's tiles.  The
     # node / triangle counts depend slightly on the schedule (which lanes run the
@@ -193,22 +198,28 @@ def main():
     sts = [shard.stats() for _ in range(max(args.stats_reps, 1))]
     st = sts[0]
 
-    # a real (non-NULL) stream: the launch, the events and the gather are ordered on it
-    stream = torch.cuda.Stream(device=dev)
-    torch.cuda.set_stream(stream)
-    frame_ids = [f for f, _ in frames]
+    # real (non-NULL) streams: a step's launch, its events and its gather are ordered on
+    # one of them.  P > 1: the context's pipeline streams (each on a hardware queue of its
+    # own), step k on stream k % P into output set k % P, so consecutive frames overlap
+    if P == 1:
+        streams = [torch.cuda.Stream(device=dev)]
+    else:
+        streams = [torch.cuda.ExternalStream(ctx.pipeline_stream(i), device=dev) for i in range(P)]
+    torch.cuda.set_stream(streams[0])
 
-    def step(ev):
-        if ev is not None:
-            ev[0].record(stream)
-        shard.launch(stream.cuda_stream)
-        if ev is not None:
-            ev[1].record(stream)
-        got = shard.gather()
+    def step(k, ev):
+        s = streams[k % P]
+        with torch.cuda.stream(s):
+            if ev is not None:
+                ev[0].record(s)
+            shard.launch(s.cuda_stream, slot=k % P)
+            if ev is not None:
+                ev[1].record(s)
+            got = shard.gather(slot=k % P)
         return got["u8"] if got is not None else None
 
-    for _ in range(args.warmup):
-        step(None)
+    for k in range(args.warmup):
+        step(k, None)
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -216,12 +227,30 @@ def main():
     t0 = time.perf_counter()
     img = None
     for k in range(args.steps):
-        img = step(evs[k])
+        img = step(k, evs[k])
     torch.cuda.synchronize()
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs])) if args.steps else 0.0
+    # per-launch time: serial steps, the event pair around each launch; pipelined, the
+    # steady-state interval between consecutive launch completions (an event pair would
+    # also count the time a launch waits for the CUs its predecessor still holds)
+    spans = [a.elapsed_time(b) for a, b in evs]
+    if P > 1 and args.steps > 1:
+        kern_ms = evs[0][1].elapsed_time(evs[-1][1]) / (args.steps - 1)
+    else:
+        kern_ms = float(np.mean(spans)) if args.steps else 0.0
+    # one more launch alone on an idle device (untimed): the single-frame latency
+    iso = None
+    if P > 1:
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(streams[0]):
+            e0.record(streams[0])
+            shard.launch(streams[0].cuda_stream, slot=0)
+            e1.record(streams[0])
+        torch.cuda.synchronize()
+        iso = e0.elapsed_time(e1)
 
     mine = np.array([elapsed, st["traced_rays"], st["queries"], st["samples"], st["node_visits"],
                      st["tri_tests"], kern_ms], np.float64)
@@ -297,6 +326,12 @@ def main():
             "samples_per_s": round(samples / max_t, 1),
             "reference_queries_per_s": round(queries / max_t, 1),
             "kernel_ms": round(kern_ms, 3),
+            "timing": {"pipeline": P,
+                       "launch_ms": round(kern_ms, 3),
+                       "launch_ms_is": "event pair around each launch" if P == 1 or args.steps < 2 else
+                       "steady-state interval between consecutive launch completions (HIP events; "
+                       f"{P} frames in flight on the context's pipeline streams)",
+                       "isolated_launch_ms": round(iso, 3) if iso is not None else round(kern_ms, 3)},
             "simt_utilisation": {k: round(v, 4) for k, v in simt.items()},
             "per_launch": {"traced_rays": int(mine[1]), "node_visits": int(mine[4]), "tri_tests": int(mine[5]),
                            "algorithmic_bytes": int(bytes_launch), "kernel": kernel,

@@ -192,12 +192,17 @@ int wgt_render_frames(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uin
 /* Tile-list launch with DEVICE buffers: n_tiles tiles of tw x th (d_tiles: device
  * array of wgt_tile) written compactly, tile after tile (out[(t*th + ly)*tw + lx]).
  * cam->seed is ignored (per-tile seeds).  Always asynchronous: the call returns
- * as soon as the launches are queued, ordered on `stream`, and after every earlier
- * launch of the same context on any stream; read the outputs only after
- * synchronising `stream`.  The one exception is the wavefront kernel family
- * (WGT_KERNEL=0, off by default), whose host loop polls a device completion
- * counter and returns when the frame is done.  wgt_upload_scene and wgt_destroy
- * wait for every launch of the context before freeing what it reads. */
+ * as soon as the launches are queued, ordered on `stream`; read the outputs only
+ * after synchronising `stream`.  The context's launches use its scheduling
+ * workspaces round-robin (2 by default, WGT_WS_SLOTS = 1..4), and a launch waits
+ * on the device only for the previous launch that used the same workspace: two
+ * consecutive calls on different streams may run concurrently (the next frame's
+ * waves fill the CUs the previous frame's end-of-launch drain leaves idle), so the
+ * caller gives such calls distinct output buffers.  The one exception is the
+ * wavefront kernel family (WGT_KERNEL=0, off by default), whose host loop polls a
+ * device completion counter and returns when the frame is done.  wgt_upload_scene
+ * and wgt_destroy wait for every launch of the context before freeing what it
+ * reads. */
 int wgt_render_tiles_async(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint32_t H,
                            uint32_t tw, uint32_t th, const wgt_tile *d_tiles, uint32_t n_tiles,
                            void *d_rgba8, float *d_rgba32f, uint32_t *d_hit_id, void *stream);
@@ -232,6 +237,10 @@ int wgt_selftest_math(wgt_ctx *ctx, uint32_t n, uint32_t seed, uint64_t counts[8
 
 /* The context's HIP stream (hipStream_t) for callers that share it. */
 void *wgt_stream(wgt_ctx *ctx);
+/* Stream i (0..3) of the context's pipeline streams, created on first use with a
+ * full CU mask so that each has a hardware queue of its own: frames issued
+ * round-robin on them overlap (wgt_render_tiles_async).  NULL on error. */
+void *wgt_pipeline_stream(wgt_ctx *ctx, uint32_t i);
 
 /* ---- host-side scene helpers (no GPU needed) ----------------------------- */
 /* Scene::Scene (scene.cpp:14-36): the reference Cornell box, 1 light, 17 quads,

@@ -171,3 +171,46 @@ def test_dist_two_ranks_vs_oracle(tmp_path, wgt, oracle, scene, scaling):
         assert np.array_equal(got[f"u8_{f}"], ref["u8"]), f
         assert np.array_equal(got[f"f32_{f}"].view(np.uint32), ref["f32"].view(np.uint32)), f
     osc.close()
+
+
+def test_pipelined_launches_vs_oracle(ctx, wgt, oracle):
+    """bench.py's pipelined steps: launches alternate over the context's two pipeline
+    streams (own hardware queues) and workspace slots, so consecutive launches run
+    concurrently.  Four launches with seeds 10..13 into four buffers, issued back to
+    back, each equal the oracle's frame of its seed bit for bit; a scene re-upload then
+    waits for all of them (wgt_upload_scene drains every slot)."""
+    import torch
+
+    L, Q, S, T = wgt.mesh_scene("bunny", target_tris=2000)
+    ctx.upload_scene(L, Q, S, T)
+    W, H, TS, spp = 100, 60, 16, 16
+    dev = torch.device("cuda", 0)
+    streams = [ctx.pipeline_stream(i) for i in range(2)]
+    assert streams[0] and streams[1] and streams[0] != streams[1]
+    assert ctx.pipeline_stream(0) == streams[0]  # created once
+    cam = wgt.camera_param(W / H, spp, 0)
+    outs, tls = [], []
+    for k in range(4):
+        tiles = wgt.tile_grid(W, H, TS, seed=10 + k)
+        d_t = torch.from_numpy(tiles.view(np.uint8).copy()).to(dev)
+        out = torch.zeros((len(tiles), TS, TS, 4), dtype=torch.float32, device=dev)
+        torch.cuda.synchronize()
+        tls.append((tiles, d_t))
+        outs.append(out)
+    for k in range(4):
+        tiles, d_t = tls[k]
+        ctx.render_tiles_async(cam, W, H, TS, TS, d_t.data_ptr(), len(tiles), d_f32=outs[k].data_ptr(),
+                               stream=streams[k % 2])
+    ctx.upload_scene(L, Q, S, T)  # must wait for the four launches before freeing the scene
+    torch.cuda.synchronize()
+    from webgputracer_amd.dist import assemble
+
+    osc = oracle.OracleScene(L, Q, S, T)
+    for k in range(4):
+        tiles, _ = tls[k]
+        img = assemble(tiles, outs[k].cpu().numpy(), W, H, TS, [0])[0]
+        ref = osc.render(oracle.camera_param(W / H, spp, 10 + k), W, H, want=("f32",))["f32"]
+        assert np.array_equal(img.view(np.uint32), ref.view(np.uint32)), k
+    osc.close()
+    with pytest.raises(Exception):
+        ctx.pipeline_stream(4)

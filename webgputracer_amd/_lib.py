@@ -63,6 +63,7 @@ EXPORTS = [
     "wgt_create", "wgt_destroy", "wgt_last_error", "wgt_version", "wgt_device_count",
     "wgt_upload_scene", "wgt_scene_info_get", "wgt_render_tile", "wgt_render_tiles_async",
     "wgt_render_tiles_stats", "wgt_render_tiles_profile", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_selftest_math", "wgt_stream",
+    "wgt_pipeline_stream",
     "wgt_scene_cornell", "wgt_make_triangles", "wgt_load_obj", "wgt_procedural_mesh",
     "wgt_write_obj", "wgt_write_png", "wgt_bvh_build", "wgt_bvh_build_compact", "wgt_render_frames",
 ]
@@ -111,6 +112,7 @@ def lib():
         "wgt_sync": (I, [P]),
         "wgt_selftest_math": (I, [P, U32, U32, P]),
         "wgt_stream": (P, [P]),
+        "wgt_pipeline_stream": (P, [P, U32]),
         "wgt_scene_cornell": (I, [P, ctypes.POINTER(U32), P, ctypes.POINTER(U32), P, ctypes.POINTER(U32)]),
         "wgt_make_triangles": (I, [P, U32, P, I, P, P]),
         "wgt_load_obj": (I, [ctypes.c_char_p, P, P, I, P, ctypes.POINTER(U32)]),

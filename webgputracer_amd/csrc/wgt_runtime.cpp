@@ -50,11 +50,26 @@ struct wgt_ctx {
   DevBuf wf, ctl;
   unsigned long long* ctl_host = nullptr;
   uint32_t ps_resident = 0;
-  DevBuf ws;  // scheduling workspace of the persistent kernel (queues, LPT costs and order)
-  // recorded after every launch that reads the scene or ws (renders on any stream and
-  // trace queries alike); each such launch first waits for the previous one, so this
-  // event completing means every earlier launch of the context has finished: the
-  // scene and ws are freed (re-upload, destroy, regrow) only after it
+  // Scheduling workspaces of the persistent kernel (queues, LPT costs and order),
+  // used round-robin by its launches.  A launch waits (on the device) only for the
+  // previous launch that used the same slot, so consecutive frames issued on two
+  // streams overlap: the next frame's pre-pass and first waves fill the CUs that the
+  // previous frame's end-of-launch drain leaves idle.
+  static constexpr int kMaxWsSlots = 4;
+  struct WsSlot {
+    DevBuf ws;
+    hipEvent_t ev = nullptr;  // recorded after the slot's last launch
+  };
+  WsSlot slots[kMaxWsSlots];
+  uint32_t next_slot = 0;
+  // wgt_pipeline_stream: streams for frames issued round-robin, each created with a
+  // full CU mask, which gives it a hardware queue of its own (two plain streams may
+  // share one, and launches on one hardware queue never overlap)
+  hipStream_t pipe[kMaxWsSlots] = {};
+  // recorded after every other launch that reads the scene (trace queries, the
+  // wavefront loop); each such launch first waits for the previous one.  The scene
+  // and the workspaces are freed (re-upload, destroy, regrow) only after this event
+  // and every slot's event have completed
   hipEvent_t use_ev = nullptr;
   std::vector<hipEvent_t> evpool;  // per-launch timing (profile runs only)
 };
@@ -87,6 +102,8 @@ int use_end(wgt_ctx* ctx, hipStream_t s) {
 // Host wait for every launch of the context (before freeing what they read).
 int use_drain(wgt_ctx* ctx) {
   if (ctx->use_ev) WGT_HIP(ctx, hipEventSynchronize(ctx->use_ev));
+  for (auto& sl : ctx->slots)
+    if (sl.ev) WGT_HIP(ctx, hipEventSynchronize(sl.ev));
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   return WGT_OK;
 }
@@ -295,15 +312,20 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
     if (timing && (!e0 || !e1)) return fail(ctx, WGT_E_HIP, "hipEventCreate failed");
     if (timing) WGT_HIP(ctx, hipEventRecord(e0, s));
     int rc;
+    // the next workspace slot: a launch on any stream first waits for the previous
+    // launch that used it (WGT_WS_SLOTS = 1 serialises every launch of the context)
+    const uint32_t n_slots = std::min<uint32_t>(std::max<uint32_t>(env_u32("WGT_WS_SLOTS", 2), 1u),
+                                                (uint32_t)wgt_ctx::kMaxWsSlots);
+    wgt_ctx::WsSlot& sl = ctx->slots[ctx->next_slot % n_slots];
+    ctx->next_slot = (ctx->next_slot + 1) % n_slots;
     const size_t ws_need = render_ws_bytes(fr);
-    if (ctx->ws.bytes < ws_need && (rc = use_drain(ctx))) return rc;  // before regrowing
-    if ((rc = ensure(ctx, ctx->ws, ws_need))) return rc;
-    // the workspace is the context's: a launch on any stream first waits for the
-    // previous launch of the context (calls on one context serialise on the device)
-    if ((rc = use_begin(ctx, s))) return rc;
+    if (sl.ws.bytes < ws_need && (rc = use_drain(ctx))) return rc;  // before regrowing
+    if ((rc = ensure(ctx, sl.ws, ws_need))) return rc;
+    if (!sl.ev) WGT_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+    else WGT_HIP(ctx, hipStreamWaitEvent(s, sl.ev, 0));
     WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
-                               ctx->ws.p, ctx->ws.bytes, s));
-    if ((rc = use_end(ctx, s))) return rc;
+                               sl.ws.p, sl.ws.bytes, s));
+    WGT_HIP(ctx, hipEventRecord(sl.ev, s));
     if (timing) {
       WGT_HIP(ctx, hipEventRecord(e1, s));
       WGT_HIP(ctx, hipEventSynchronize(e1));
@@ -419,7 +441,17 @@ void wgt_destroy(wgt_ctx* ctx) {
   if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
   free_buf(ctx->tiles); free_buf(ctx->out8); free_buf(ctx->out32); free_buf(ctx->hit);
   free_buf(ctx->counters); free_buf(ctx->rays); free_buf(ctx->prim); free_buf(ctx->dist);
-  free_buf(ctx->wf); free_buf(ctx->ctl); free_buf(ctx->ws);
+  free_buf(ctx->wf); free_buf(ctx->ctl);
+  for (auto& sl : ctx->slots) {
+    if (sl.ev) (void)hipEventSynchronize(sl.ev);
+    free_buf(sl.ws);
+    if (sl.ev) (void)hipEventDestroy(sl.ev);
+  }
+  for (hipStream_t& p : ctx->pipe) {
+    if (p) (void)hipStreamSynchronize(p);
+    if (p) (void)hipStreamDestroy(p);
+    p = nullptr;
+  }
   if (ctx->use_ev) (void)hipEventDestroy(ctx->use_ev);
   if (ctx->ctl_host) (void)hipHostFree(ctx->ctl_host);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
@@ -430,6 +462,27 @@ void wgt_destroy(wgt_ctx* ctx) {
 }
 
 void* wgt_stream(wgt_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+void* wgt_pipeline_stream(wgt_ctx* ctx, uint32_t i) {
+  if (!ctx || i >= (uint32_t)wgt_ctx::kMaxWsSlots) {
+    (void)fail(ctx, WGT_E_INVALID, "pipeline stream index out of range");
+    return nullptr;
+  }
+  if (!ctx->pipe[i]) {
+    if (hipSetDevice(ctx->device) != hipSuccess) return nullptr;
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess || cus <= 0)
+      return nullptr;
+    std::vector<uint32_t> mask(((size_t)cus + 31) / 32, 0xffffffffu);
+    const hipError_t e = hipExtStreamCreateWithCUMask(&ctx->pipe[i], (uint32_t)mask.size(), mask.data());
+    if (e != hipSuccess) {
+      ctx->pipe[i] = nullptr;
+      (void)fail(ctx, WGT_E_HIP, std::string("hipExtStreamCreateWithCUMask: ") + hipGetErrorString(e));
+      return nullptr;
+    }
+  }
+  return (void*)ctx->pipe[i];
+}
 
 int wgt_sync(wgt_ctx* ctx) {
   if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");

@@ -115,9 +115,13 @@ class ShardedFrames:
     copies) and rank 0's assembly with a single index op built once here.
 
     frames: list of (frame id, seed).  want: "u8" (rgba8, always) and optionally
-    "f32" (radiance before quantisation, gathered the same way)."""
+    "f32" (radiance before quantisation, gathered the same way).  depth: output
+    buffer sets, one per step in flight: consecutive steps launched on different
+    streams (the context's pipeline streams) overlap on the device, so step k
+    renders into set k % depth (launch(stream, slot), gather(slot))."""
 
-    def __init__(self, ctx, cam, W, H, T, frames, rank, world, dist, device, backend="nccl", want=("u8",)):
+    def __init__(self, ctx, cam, W, H, T, frames, rank, world, dist, device, backend="nccl", want=("u8",),
+                 depth=1):
         import torch
 
         self.ctx, self.cam, self.W, self.H, self.T = ctx, cam, W, H, T
@@ -126,9 +130,13 @@ class ShardedFrames:
         self.tiles = shard_tiles(W, H, T, self.frames, rank, world)
         self.n_max = max_tiles_per_rank(W, H, T, len(self.frames), world)
         self.d_tiles = torch.from_numpy(self.tiles.view(np.uint8).copy()).to(device)
-        self.bufs = {"u8": torch.zeros((self.n_max, T, T, 4), dtype=torch.uint8, device=device)}
-        if "f32" in want:
-            self.bufs["f32"] = torch.zeros((self.n_max, T, T, 4), dtype=torch.float32, device=device)
+        self.bufsets = []
+        for _ in range(max(depth, 1)):
+            b = {"u8": torch.zeros((self.n_max, T, T, 4), dtype=torch.uint8, device=device)}
+            if "f32" in want:
+                b["f32"] = torch.zeros((self.n_max, T, T, 4), dtype=torch.float32, device=device)
+            self.bufsets.append(b)
+        self.bufs = self.bufsets[0]
         self.frame_ids = [f for f, _ in self.frames]
         self.asm_idx = None
         if rank == 0:
@@ -141,20 +149,23 @@ class ShardedFrames:
         return self.ctx.render_tiles_stats(self.cam, self.W, self.H, self.T, self.T, self.d_tiles.data_ptr(),
                                            len(self.tiles))
 
-    def launch(self, stream=0):
-        """Render this rank's tiles (asynchronous, ordered on `stream`, a raw hipStream_t)."""
-        f32 = self.bufs.get("f32")
+    def launch(self, stream=0, slot=0):
+        """Render this rank's tiles into buffer set `slot` (asynchronous, ordered on `stream`, a raw
+        hipStream_t)."""
+        bufs = self.bufsets[slot]
+        f32 = bufs.get("f32")
         self.ctx.render_tiles_async(self.cam, self.W, self.H, self.T, self.T, self.d_tiles.data_ptr(),
-                                    len(self.tiles), d_u8=self.bufs["u8"].data_ptr(),
+                                    len(self.tiles), d_u8=bufs["u8"].data_ptr(),
                                     d_f32=f32.data_ptr() if f32 is not None else 0, stream=stream)
 
-    def gather(self):
-        """Gather every rank's tiles to rank 0 and assemble: {kind: {frame id: (H, W, 4) tensor}}
-        on rank 0, None elsewhere."""
+    def gather(self, slot=0):
+        """Gather every rank's tiles of buffer set `slot` to rank 0 and assemble (on torch's current
+        stream, which must be the one the launch ran on): {kind: {frame id: (H, W, 4) tensor}} on
+        rank 0, None elsewhere."""
         import torch
 
         out = {}
-        for kind, buf in self.bufs.items():
+        for kind, buf in self.bufsets[slot].items():
             got = gather_tiles(buf if self.backend == "nccl" else buf.cpu(), self.rank, self.world, self.dist)
             if self.rank == 0:
                 data = (got[0] if self.world == 1 else torch.cat(got)).to(self.device).reshape(-1, 4)

@@ -16,7 +16,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import (CAMERA_DTYPE, QUAD_DTYPE, SPHERE_DTYPE, TILE_DTYPE, TRI_DTYPE, WgtSceneInfo, WgtStats,
-                   check, lib, ptr)
+                   WGT_E_HIP, WgtError, check, lib, ptr)
 
 COL_WHITE = np.array([0.73, 0.73, 0.73], np.float32)  # color_util.h:8
 MESH_KINDS = {"bunny": (0, 69451), "sponza": (1, 262267)}
@@ -234,6 +234,13 @@ class Context:
 
     def stream(self) -> int:
         return self._L.wgt_stream(self.h) or 0
+
+    def pipeline_stream(self, i: int) -> int:
+        """The context's i-th pipeline stream (own hardware queue; frames issued round-robin overlap)."""
+        s = self._L.wgt_pipeline_stream(self.h, i)
+        if not s:
+            raise WgtError(WGT_E_HIP, (self._L.wgt_last_error(self.h) or b"").decode())
+        return s
 
     def sync(self):
         self._check(self._L.wgt_sync(self.h))
