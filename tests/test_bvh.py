@@ -207,10 +207,11 @@ def test_compact_nodes_full_size_meshes():
 
 
 def test_narrow_tree_selects_six_waves(monkeypatch):
-    """A tree that collapses under the 25-entry stack bound at <= 3% more nodes is
-    kept narrow, and the persistent kernel runs 6 waves per SIMD on it (bunny
-    stand-in: 17,791 vs 17,637 nodes); sponza's would grow 26%, so it keeps the
-    31-entry bound and 5 waves.  WGT_PS_WAVES=5 keeps every tree wide."""
+    """A tree that collapses under the 25-entry stack bound at <= 3% more SAH cost
+    (greedy collapse: nodes) is kept narrow, and the persistent kernel runs 6 waves
+    per SIMD on it (bunny stand-in: SAH-optimal trees of cost 22.77 at 25 entries vs
+    22.63 at 31); sponza's would cost 5% more, so it keeps the 31-entry bound and 5
+    waves.  WGT_PS_WAVES=5 keeps every tree wide."""
     bunny = w.procedural_mesh("bunny", 20000)
     info = check_tree(bunny)  # the exported (= uploaded) tree passes the full walk
     assert info["ps_waves"] == 6 and info["bvh_stack"] <= 25
@@ -221,3 +222,44 @@ def test_narrow_tree_selects_six_waves(monkeypatch):
     monkeypatch.setenv("WGT_PS_WAVES", "5")
     info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
     assert info["ps_waves"] == 5 and info["bvh_stack"] == 31
+
+
+def bvh4_sah(nodes):
+    """SAH cost of an exported BVH4 (root-relative): the root plus every internal child's box
+    area (node visits), and count x area of every leaf child (triangle tests)."""
+    N = nodes.reshape(-1, 8, 4).astype(np.float64)
+    refs = nodes.reshape(-1, 8, 4)[:, 6, :].view(np.int32)
+    lx, hx, ly, hy, lz, hz = (N[:, i, :] for i in range(6))
+    live = ~((lx == np.float64(EMPTY)) & (hx == np.float64(EMPTY)))
+    dx, dy, dz = np.maximum(hx - lx, 0), np.maximum(hy - ly, 0), np.maximum(hz - lz, 0)
+    area = 2 * (dx * dy + dy * dz + dz * dx) * live
+    r = live[0]
+    ext = [hx[0][r].max() - lx[0][r].min(), hy[0][r].max() - ly[0][r].min(), hz[0][r].max() - lz[0][r].min()]
+    ra = 2 * (ext[0] * ext[1] + ext[1] * ext[2] + ext[2] * ext[0])
+    inner, leaf = (refs >= 0) & live, (refs < 0) & live
+    cnt = ((~refs) & 7) + 1
+    return 1.0 + area[inner].sum() / ra, (area[leaf] * cnt[leaf]).sum() / ra
+
+
+@pytest.mark.parametrize("leaf", ["0", "8"])
+def test_optimal_collapse_vs_greedy(monkeypatch, leaf):
+    """The SAH-optimal collapse (default, WGT_COLLAPSE=dp) exports a tree that passes the full
+    walk (containment, leaf partition, exact stack need), and at the same stack bound its
+    node-visit SAH is never above the greedy collapse's (WGT_COLLAPSE=greedy); with leaf
+    merging off (WGT_DP_LEAF=0) the leaves are the same, so the triangle SAH is equal."""
+    monkeypatch.setenv("WGT_PS_WAVES", "5")  # both at the 31-entry bound
+    monkeypatch.setenv("WGT_DP_LEAF", leaf)
+    for tris in (random_soup(3000, 5), w.procedural_mesh("bunny", 20000)):
+        monkeypatch.setenv("WGT_COLLAPSE", "greedy")
+        g_info, g_nodes, _ = w.bvh_build(tris)
+        monkeypatch.setenv("WGT_COLLAPSE", "dp")
+        d_info = check_tree(tris)
+        _, d_nodes, _ = w.bvh_build(tris)
+        gn, gt = bvh4_sah(g_nodes)
+        dn, dt = bvh4_sah(d_nodes)
+        if leaf == "0":
+            assert dn <= gn * (1 + 1e-6), (dn, gn)
+            assert abs(dt - gt) <= 1e-6 * gt
+        else:
+            assert dn + dt <= (gn + gt) * (1 + 1e-6), (dn + dt, gn + gt)
+        assert d_info["bvh_stack"] <= STACK_MAX

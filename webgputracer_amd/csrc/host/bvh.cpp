@@ -11,6 +11,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <limits>
+#include <memory>
 
 #include "../wgt_geom.h"
 
@@ -315,6 +316,181 @@ class Collapser {
   std::vector<uint32_t> h_;  // BVH2 height (internal levels) of every BVH2 node
 };
 
+// SAH-optimal collapse under the stack budget (the default; WGT_COLLAPSE=greedy
+// selects Collapser).  Every BVH4 node is a frontier of 2..4 descendants of a BVH2
+// node; a dynamic program over the BVH2 (children before parents) picks, per node
+// and per stack budget B, the frontier minimising the BVH4 SAH cost
+//   N(r, B) = c_node * A(r) + min_{k=2..4} Q(r's children -> k slots, B - (k - 1))
+//   Q(c -> 1 slot, B) = leaf ? c_tri * count * A(c) : N(c, B)
+//   Q(c -> k slots, B) = min_{i + j = k} Q(left(c) -> i, B) + Q(right(c) -> j, B)
+// (A = surface area; a node of k slots pushes at most k - 1 entries, so its
+// subtree's stack need is (k - 1) + the largest need of its internal slots).
+// Like the greedy collapse it only regroups BVH2 boxes: the BVH4 child boxes are
+// BVH2 node boxes and the exactness argument is unchanged.
+double DpNodeCost() {
+  const char* v = std::getenv("WGT_DP_NODE");
+  return v && *v ? std::atof(v) : 1.0;
+}
+double DpTriCost() {
+  const char* v = std::getenv("WGT_DP_TRI");
+  return v && *v ? std::atof(v) : 1.0;
+}
+// Largest leaf the collapse may make of a BVH2 subtree (its triangles are one
+// contiguous range): 0 keeps the BVH2 leaves (WGT_DP_LEAF, <= kLeafMax).
+uint32_t DpLeafMax() {
+  const char* v = std::getenv("WGT_DP_LEAF");
+  const int n = v && *v ? std::atoi(v) : 0;
+  return (uint32_t)std::max(0, std::min(n, kLeafMax));
+}
+bool UseDpCollapse() {
+  const char* v = std::getenv("WGT_COLLAPSE");
+  return !(v && std::strcmp(v, "greedy") == 0);
+}
+
+class DpCollapser {
+ public:
+  DpCollapser(const std::vector<float>& n2, BvhOut& o, uint32_t budget)
+      : n2_(n2), out_(&o), nb_(budget + 1), n_(n2.size() / 16) {
+    const float inf = std::numeric_limits<float>::infinity();
+    cost_.assign(n_ * 4 * nb_, inf);  // [node][k-1][B]: k = 1 is N(node, B)
+    range_.assign(n_, Range{0u, 0u});
+    area_.assign(n_, 0.0);
+    for (size_t i = n_; i-- > 0;) {   // preorder: children have larger ids
+      const Child a = Child2(n2_, (int)i, 0), b = Child2(n2_, (int)i, 1);
+      Box u = a.b;
+      u.grow(b.b);
+      const double area = u.area();
+      area_[i] = area;
+      // the node's triangles: one contiguous range (the children's ranges are adjacent)
+      const Range ra = Tris(a), rb = Tris(b);
+      range_[i] = Range{std::min(ra.first, rb.first), ra.count + rb.count};
+      for (uint32_t B = 0; B < nb_; ++B) {
+        // k slots of node i's frontier, each with need <= B
+        for (int k = 2; k <= 4; ++k) {
+          float best = inf;
+          for (int ia = 1; ia < k; ++ia) best = std::min(best, Slots(a, ia, B) + Slots(b, k - ia, B));
+          Q(i, k, B) = best;
+        }
+        float best = inf;
+        for (int k = 2; k <= 4; ++k)
+          if ((uint32_t)(k - 1) <= B) best = std::min(best, Q(i, k, B - (uint32_t)(k - 1)));
+        Q(i, 1, B) = (float)(c_node_ * area) + best;
+      }
+    }
+  }
+  float Cost(uint32_t budget) const { return budget < nb_ ? Q(0, 1, budget) : std::numeric_limits<float>::infinity(); }
+  void Retarget(BvhOut& o) { out_ = &o; }
+
+  // Emit node id2 as a BVH4 node with stack need <= budget (preorder ids).
+  int Emit(int id2, uint32_t depth, uint32_t budget, uint32_t& need) {
+    const Child a = Child2(n2_, id2, 0), b = Child2(n2_, id2, 1);
+    int best_k = 2;
+    float best = std::numeric_limits<float>::infinity();
+    for (int k = 2; k <= 4; ++k)
+      if ((uint32_t)(k - 1) <= budget && Q(id2, k, budget - (uint32_t)(k - 1)) < best) {
+        best = Q(id2, k, budget - (uint32_t)(k - 1));
+        best_k = k;
+      }
+    const uint32_t sb = budget - (uint32_t)(best_k - 1);
+    std::vector<Child> slots;
+    Split(a, b, best_k, sb, slots);
+    BvhOut& out = *out_;
+    const uint32_t id = (uint32_t)(out.nodes.size() / kNode4Floats);
+    out.nodes.resize(out.nodes.size() + kNode4Floats);
+    out.max_depth = std::max(out.max_depth, depth + 1);
+    const int n = (int)slots.size();
+    int refs[kBvhWidth];
+    uint32_t sub = 0;
+    for (int i = 0; i < n; ++i) {
+      if (slots[i].ref >= 0) {
+        uint32_t sn = 0;
+        refs[i] = Emit(slots[i].ref, depth + 1, sb, sn);
+        sub = std::max(sub, sn);
+      } else {
+        refs[i] = slots[i].ref;
+      }
+    }
+    need = (uint32_t)(n - 1) + sub;
+    float* o = &out.nodes[(size_t)id * kNode4Floats];
+    for (int i = 0; i < kBvhWidth; ++i) {
+      const bool live = i < n;
+      for (int c = 0; c < 3; ++c) {
+        o[(2 * c) * 4 + i] = live ? slots[i].b.lo[c] : kEmptySlotCoord;
+        o[(2 * c + 1) * 4 + i] = live ? slots[i].b.hi[c] : kEmptySlotCoord;
+      }
+      const int r = live ? refs[i] : refs[0];
+      std::memcpy(&o[24 + i], &r, 4);
+      o[28 + i] = 0.0f;
+    }
+    return (int)id;
+  }
+
+ private:
+  float& Q(size_t node, int k, uint32_t B) { return cost_[(node * 4 + (size_t)(k - 1)) * nb_ + B]; }
+  float Q(size_t node, int k, uint32_t B) const { return cost_[(node * 4 + (size_t)(k - 1)) * nb_ + B]; }
+  // cost of covering child c with k slots, each of stack need <= B
+  float Slots(const Child& c, int k, uint32_t B) const {
+    if (c.ref < 0) return k == 1 ? (float)(c_tri_ * leaf_count(c.ref) * c.b.area()) : std::numeric_limits<float>::infinity();
+    if (k == 1 && Mergeable(c)) return std::min(Q((size_t)c.ref, 1, B), MergedCost(c));
+    return Q((size_t)c.ref, k, B);
+  }
+  struct Range {
+    uint32_t first, count;
+  };
+  Range Tris(const Child& c) const {
+    if (c.ref < 0) return Range{leaf_first(c.ref), leaf_count(c.ref)};
+    return range_[(size_t)c.ref];
+  }
+  // an internal BVH2 child with few enough triangles may become one leaf slot
+  bool Mergeable(const Child& c) const {
+    if (c.ref < 0 || leaf_max_ == 0) return false;
+    const uint32_t n = range_[(size_t)c.ref].count;
+    return n != 0 && n <= leaf_max_;
+  }
+  float MergedCost(const Child& c) const { return (float)(c_tri_ * range_[(size_t)c.ref].count * area_[(size_t)c.ref]); }
+  // the slot of child c in a cover by one slot: merged into a leaf when that is cheaper
+  Child AsSlot(const Child& c, uint32_t B) const {
+    if (Mergeable(c) && MergedCost(c) < Q((size_t)c.ref, 1, B)) {
+      const Range r = range_[(size_t)c.ref];
+      Child m = c;
+      m.ref = leaf_ref(r.first, r.count);
+      return m;
+    }
+    return c;
+  }
+  // the slots of the cheapest cover of a and b by k slots (budget B each)
+  void Split(const Child& a, const Child& b, int k, uint32_t B, std::vector<Child>& out) const {
+    int best_i = 1;
+    float best = std::numeric_limits<float>::infinity();
+    for (int i = 1; i < k; ++i) {
+      const float c = Slots(a, i, B) + Slots(b, k - i, B);
+      if (c < best) {
+        best = c;
+        best_i = i;
+      }
+    }
+    Cover(a, best_i, B, out);
+    Cover(b, k - best_i, B, out);
+  }
+  void Cover(const Child& c, int k, uint32_t B, std::vector<Child>& out) const {
+    if (k == 1) {
+      out.push_back(AsSlot(c, B));
+      return;
+    }
+    Split(Child2(n2_, c.ref, 0), Child2(n2_, c.ref, 1), k, B, out);
+  }
+
+  const std::vector<float>& n2_;
+  BvhOut* out_;
+  uint32_t nb_;
+  size_t n_;
+  double c_node_ = DpNodeCost(), c_tri_ = DpTriCost();
+  uint32_t leaf_max_ = DpLeafMax();
+  std::vector<float> cost_;
+  std::vector<Range> range_;
+  std::vector<double> area_;
+};
+
 // Compact form of one node (wgt_geom.h): lo codes are the largest binary16
 // value (bit patterns of non-negative halves order like their values) whose
 // decoded plane is <= the exact bound, hi codes the smallest whose plane is >= it.
@@ -438,7 +614,14 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
           std::to_string(stack_limit);
     return false;
   }
-  greedy.Collapse(0, 0, stack_limit, out.stack_need);
+  const bool dp = UseDpCollapse();
+  std::unique_ptr<DpCollapser> opt;
+  if (dp) {
+    opt.reset(new DpCollapser(n2, out, stack_limit));
+    if (!(opt->Cost(stack_limit) < std::numeric_limits<float>::infinity())) opt.reset();
+  }
+  if (opt) opt->Emit(0, 0, stack_limit, out.stack_need);
+  else greedy.Collapse(0, 0, stack_limit, out.stack_need);
   if (out.stack_need > stack_limit) {
     err = "BuildBvh: traversal stack " + std::to_string(out.stack_need) + " exceeds " +
           std::to_string(stack_limit);
@@ -447,10 +630,19 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
   out.n_nodes = (uint32_t)(out.nodes.size() / kNode4Floats);
   if (narrow_limit > 0 && narrow_limit < stack_limit && greedy.Height(0) <= narrow_limit) {
     BvhOut nar;
-    Collapser tight(n2, nar);
-    tight.Collapse(0, 0, narrow_limit, nar.stack_need);
+    if (opt && opt->Cost(narrow_limit) < std::numeric_limits<float>::infinity()) {
+      opt->Retarget(nar);
+      opt->Emit(0, 0, narrow_limit, nar.stack_need);
+    } else {
+      Collapser tight(n2, nar);
+      tight.Collapse(0, 0, narrow_limit, nar.stack_need);
+    }
     const uint32_t nn = (uint32_t)(nar.nodes.size() / kNode4Floats);
-    if (nar.stack_need <= narrow_limit && nn <= narrow_ratio * out.n_nodes) {
+    // greedy trees: at most narrow_ratio x the nodes; optimal trees: at most narrow_ratio
+    // x the SAH cost of the wide tree
+    const bool cheap = opt ? opt->Cost(narrow_limit) <= narrow_ratio * opt->Cost(stack_limit)
+                           : nn <= narrow_ratio * out.n_nodes;
+    if (nar.stack_need <= narrow_limit && cheap) {
       out.nodes.swap(nar.nodes);
       out.n_nodes = nn;
       out.stack_need = nar.stack_need;
