@@ -49,7 +49,7 @@ constexpr int kMaxBins = 256;
 // SAH bins per axis (WGT_SAH_BINS, <= kMaxBins; tuning sweeps)
 int SahBins() {
   const char* v = std::getenv("WGT_SAH_BINS");
-  const int n = v && *v ? std::atoi(v) : 32;
+  const int n = v && *v ? std::atoi(v) : 128;
   return std::max(2, std::min(n, kMaxBins));
 }
 
@@ -496,7 +496,7 @@ class DpCollapser {
 // decoded plane is <= the exact bound, hi codes the smallest whose plane is >= it.
 float CDec(uint32_t h, float s, float org) { return qdec(half_bits_to_float(h), s, org); }
 void CompactNode(const float* n, float s, uint32_t* q) {
-  uint32_t meta = 0;
+  const uint32_t meta = 0;  // reserved
   bool live[kBvhWidth];
   for (int i = 0; i < kBvhWidth; ++i) live[i] = !(n[i] == kEmptySlotCoord && n[4 + i] == kEmptySlotCoord);
   float org[3];
@@ -507,8 +507,7 @@ void CompactNode(const float* n, float s, uint32_t* q) {
     org[a] = ulo;
     uint32_t lo_h[kBvhWidth], hi_h[kBvhWidth];
     for (int i = 0; i < kBvhWidth; ++i) {
-      lo_h[i] = 0x7bffu;  // an empty slot: inverted box, masked anyway
-      hi_h[i] = 0u;
+      lo_h[i] = hi_h[i] = 0x7c00u;  // an empty slot: +inf planes on every axis, never entered
       if (!live[i]) continue;
       const float blo = n[(2 * a) * 4 + i], bhi = n[(2 * a + 1) * 4 + i];
       uint32_t l = 0, r = 0x7bffu;  // largest h with CDec(h) <= blo (CDec(0) = ulo <= blo)
@@ -529,8 +528,6 @@ void CompactNode(const float* n, float s, uint32_t* q) {
     q[4 + 4 * a + 2] = hi_h[0] | (hi_h[1] << 16);
     q[4 + 4 * a + 3] = hi_h[2] | (hi_h[3] << 16);
   }
-  for (int i = 0; i < kBvhWidth; ++i)
-    if (!live[i]) meta |= 1u << (24 + i);
   std::memcpy(&q[0], org, 12);
   q[3] = meta;
 }

@@ -202,9 +202,10 @@ __device__ __forceinline__ float hcode(uint32_t w, uint32_t slot) {
 // Compact node: per axis the ray's entry plane is the lo code for inv >= 0 and the
 // hi code for inv < 0 (one select per two children), which equals the min / max
 // form of child_key because the slab formula is monotone in the plane.  The
-// decode fma(h, s, org) takes h from a half word (v_fma_mix_f32).
+// decode fma(h, s, org) takes h from a half word (v_fma_mix_f32).  An empty slot's
+// +inf codes give n = +inf or f = -inf: a miss without a mask (wgt_geom.h).
 __device__ __forceinline__ uint32_t cchild_key(const Trav& t, const uint32_t* nw, const uint32_t* fw, f3 org,
-                                               float s, uint32_t meta, uint32_t slot) {
+                                               float s, uint32_t slot) {
   const uint32_t k = slot >> 1;
   const float tnx = __builtin_fmaf(qdec(hcode(nw[0 + k], slot), s, org.x), t.inv.x, t.ot.x);
   const float tfx = __builtin_fmaf(qdec(hcode(fw[0 + k], slot), s, org.x), t.inv.x, t.ot.x);
@@ -214,8 +215,7 @@ __device__ __forceinline__ uint32_t cchild_key(const Trav& t, const uint32_t* nw
   const float tfz = __builtin_fmaf(qdec(hcode(fw[4 + k], slot), s, org.z), t.inv.z, t.ot.z);
   const float n = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, kRayMin));
   const float f = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, t.bt));
-  const bool hit = n <= f && ((meta >> (24u + slot)) & 1u) == 0u;
-  return hit ? ((__float_as_uint(n) & ~3u) | slot) : kMissKey;
+  return n <= f ? ((__float_as_uint(n) & ~3u) | slot) : kMissKey;
 }
 template <bool CN>
 __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int ref, uint32_t& k0, uint32_t& k1,
@@ -226,7 +226,6 @@ __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int
     const float4 a = n[0];
     const uint4 x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]),
                 z = __builtin_bit_cast(uint4, n[3]);
-    const uint32_t meta = __float_as_uint(a.w);
     const f3 org = f3{a.x, a.y, a.z};
     const bool sx = t.inv.x < 0.0f, sy = t.inv.y < 0.0f, sz = t.inv.z < 0.0f;
     const uint32_t nw[6] = {sx ? x.z : x.x, sx ? x.w : x.y, sy ? y.z : y.x,
@@ -234,10 +233,10 @@ __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int
     const uint32_t fw[6] = {sx ? x.x : x.z, sx ? x.y : x.w, sy ? y.x : y.z,
                             sy ? y.y : y.w, sz ? z.x : z.z, sz ? z.y : z.w};
     r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
-    k0 = cchild_key(t, nw, fw, org, sc.cstep, meta, 0u);
-    k1 = cchild_key(t, nw, fw, org, sc.cstep, meta, 1u);
-    k2 = cchild_key(t, nw, fw, org, sc.cstep, meta, 2u);
-    k3 = cchild_key(t, nw, fw, org, sc.cstep, meta, 3u);
+    k0 = cchild_key(t, nw, fw, org, sc.cstep, 0u);
+    k1 = cchild_key(t, nw, fw, org, sc.cstep, 1u);
+    k2 = cchild_key(t, nw, fw, org, sc.cstep, 2u);
+    k3 = cchild_key(t, nw, fw, org, sc.cstep, 3u);
   } else {
     const float4* __restrict__ n = sc.nodes + 8 * ref;
     const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];

@@ -108,8 +108,11 @@ constexpr int kLeafMax = 8;
 // binary16 code h >= 0, decoded as qdec(h, s, org_a) = fma(h, s, org_a) (one
 // rounding of an exact product, monotone in h) with one scene-wide power-of-two
 // step s:
-//   C[0] = (org.x, org.y, org.z, meta)   org = lower bounds of the children's
-//          union; meta bits 24..27: slot i empty (masked: never entered)
+//   C[0] = (org.x, org.y, org.z, 0)      org = lower bounds of the children's
+//          union
+//   an empty slot has the code +inf (0x7c00) for every plane: whatever the sign
+//   of 1/d (finite and nonzero, safe_inv), its entry distance is +inf or its
+//   exit distance -inf, so the slab test rejects it and it is never entered
 //   C[1] = lo.x of children (0|1, 2|3 as half pairs), hi.x (0|1, 2|3)
 //   C[2] = lo.y, hi.y                     C[3] = lo.z, hi.z
 //   C[4] = child refs (int bits), as N[6]
