@@ -176,10 +176,10 @@ __device__ __forceinline__ void trav_init(f3 o, f3 d, bool quad_hit, float qt, T
 }
 
 
-// Sort key of one BVH4 child: the clamped entry distance max(near, kRayMin)
-// (positive, so its bits order as unsigned) with the slot in the low 2 bits;
-// kMissKey if the ray misses the box or the box lies beyond the current closest
-// hit.  hit = max(near, kRayMin) <= min(far, bt) is the node test
+// Sort key of one BVH4 child: the bits of the clamped entry distance max(near,
+// kRayMin) (positive and not NaN, so its bits order as unsigned and never equal
+// kMissKey); kMissKey if the ray misses the box or the box lies beyond the current
+// closest hit.  Equal keys sort in either order (the ref moves with its key).  hit = max(near, kRayMin) <= min(far, bt) is the node test
 // near <= far && near <= bt && far >= kRayMin, because bt >= kRayMin always
 // (bt is kRayMax, a quad t or a triangle t, all >= kRayMin).
 constexpr uint32_t kMissKey = 0xFFFFFFFFu;
@@ -192,7 +192,7 @@ __device__ __forceinline__ uint32_t child_key(const Trav& t, float lx, float hx,
                                   __builtin_fmaxf(__builtin_fminf(t0z, t1z), kRayMin));
   const float f = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t0x, t1x), __builtin_fmaxf(t0y, t1y)),
                                   __builtin_fminf(__builtin_fmaxf(t0z, t1z), t.bt));
-  return n <= f ? ((__float_as_uint(n) & ~3u) | slot) : kMissKey;
+  return n <= f ? __float_as_uint(n) : kMissKey;
 }
 // Sort keys and refs of the 4 children of node `ref`, read from the 128-B nodes
 // (CN = false) or from the compact nodes (CN = true, wgt_geom.h).
@@ -215,7 +215,7 @@ __device__ __forceinline__ uint32_t cchild_key(const Trav& t, const uint32_t* nw
   const float tfz = __builtin_fmaf(qdec(hcode(fw[4 + k], slot), s, org.z), t.inv.z, t.ot.z);
   const float n = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, kRayMin));
   const float f = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, t.bt));
-  return n <= f ? ((__float_as_uint(n) & ~3u) | slot) : kMissKey;
+  return n <= f ? __float_as_uint(n) : kMissKey;
 }
 template <bool CN>
 __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int ref, uint32_t& k0, uint32_t& k1,
