@@ -44,12 +44,30 @@ def main():
     bench = open(os.path.join(src, "bench.log")).read().strip().splitlines()[-1]
     line = json.loads(bench)
     out = [f"# {rnd} profile `{tag}` — {line['config']['workload']}", "",
-           "rocprofv3 --kernel-trace --stats (same bench command, 2 timed steps):", "", "| kernel | calls | avg ms |",
+           "rocprofv3 --kernel-trace --stats (same bench command, 4 timed steps, 2 frames in flight):", "", "| kernel | calls | avg ms |",
            "|---|---|---|"]
     for r in csv.DictReader(open(os.path.join(src, "kt", "run_kernel_stats.csv"))):
         if "wgt::" in r["Name"]:
             out.append(f"| `{r['Name'].split('(')[0].replace('void ', '')}` | {r['Calls']} | "
                        f"{float(r['AverageNs']) / 1e6:.3f} |")
+    # pipelined launches overlap, so a dispatch's begin-to-end also counts the time its waves
+    # waited for the CUs the previous frame still held: the per-launch figure to compare with
+    # the bench's kernel_ms is the interval between consecutive completions of the main kernel
+    kt = os.path.join(src, "kt", "run_kernel_trace.csv")
+    if os.path.exists(kt):
+        rows = [r for r in csv.DictReader(open(kt)) if "wgt::" in r["Kernel_Name"]]
+        main_k = line["per_launch"]["kernel"]
+        ends, durs = [], []
+        for r in rows:
+            if r["Kernel_Name"].split("(")[0].replace("void ", "") == main_k:
+                ends.append(int(r["End_Timestamp"]))
+                durs.append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6)
+        ends.sort()
+        if len(ends) >= 3:
+            gaps = [(b - a) / 1e6 for a, b in zip(ends, ends[1:])]
+            out += ["", f"kernel trace, `{main_k}` ({len(ends)} launches: warm-up, timed, isolated): dispatch "
+                        f"begin-to-end ms {[round(d, 1) for d in durs]}; intervals between consecutive "
+                        f"completions ms {[round(g, 1) for g in gaps]}"]
     out += ["", f"bench.py line: value {line['value']} {line['unit']}, kernel_ms {line['kernel_ms']}, "
                 f"roofline {json.dumps(line['roofline'])}", "", "PMC (separate passes, 1 timed step each):", "",
             "| kernel | counter | value per launch |", "|---|---|---|"]
