@@ -7,13 +7,18 @@ Cornell box + light, 1920x1080, 256 spp.  `--scene bunny` runs configs[2] (C3). 
 "step" renders one 1080p/256spp frame per GPU: the step's N frames are cut into 32x32
 tiles dealt round-robin over the N ranks (one process per GPU), then the tiles are
 gathered to rank 0 (RCCL over xGMI) and assembled — weak scaling, per-GPU work fixed.
+Steps are issued two deep (--pipeline 2): step k runs on the context's pipeline stream
+k % 2 into output set k % 2, so each frame starts in the previous frame's end-of-launch
+drain; every frame is still rendered whole.
 
 value = closest-hit queries actually traced (non-NaN rays, counted on the device by
 an instrumented pass over the same tiles) summed over ranks x steps / max-over-ranks
 wall time of the K timed steps.  Scene/BVH upload and tile lists are resident in HBM
-before timing.  The render call is launched on torch's current stream so
-torch.cuda.Event pairs time exactly its launches (roofline.achieved): the 1-spp cost
-pre-pass + LPT ordering (~0.5 % of the call at 256 spp) and the main kernel
+before timing.  Each render call is launched on its step's stream, where HIP events
+bracket it; with frames in flight the per-launch time (roofline.achieved) is the
+interval between consecutive launch completions (a launch's own event pair would also
+count the time it waits for the previous frame's CUs), with --pipeline 1 the event pair:
+the 1-spp cost pre-pass + LPT ordering (~1 % of the call at 256 spp) and the main kernel
 k_render_ps (the rocprof kernel trace under profiles/ lists them separately).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scene sponza|bunny|cornell]
