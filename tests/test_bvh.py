@@ -145,44 +145,56 @@ def test_bvh_stack_budget_below_height_fails(monkeypatch):
 
 
 def check_compact(tris):
-    """The compact node form (wgt_geom.h) of the same tree: every live child box
-    decodes (fma(h, step, org), exact product + one rounding, as numpy f32 h*step + org)
-    to a box containing the 128-B child box, each code is the tightest such
-    binary16 value, empty slots have +inf codes on every plane (never entered), refs are
-    the 128-B node's refs."""
+    """The compact node form (wgt_geom.h) of the same tree.  The kernel's fused slab step
+    fma(h, s/d, fma(org/s, s/d, ot)) rounds differently from the exact fma(b, 1/d, ot), so
+    every live child plane org' + h*s (org' = stored org/s times s) keeps the margin
+    G = 2^-21 M from the 128-B child bound (lo planes <= lo - G, hi planes >= hi + G),
+    with M = max(4 x the triangles' extent, 2 x every node coordinate) (BuildBvh's
+    origin_bound for the host export); each code is the tightest such binary16 value,
+    org' is the largest value of its form <= the union's lower bound - G, empty slots
+    have +inf codes on every plane (never entered), and refs are the 128-B node's refs."""
     info, nodes, _ = w.bvh_build(tris)
     cn, cr, step = w.bvh_build_compact(tris)
     step = f32(step)
     assert step > 0 and np.log2(step) == np.round(np.log2(step))  # a power of two
     assert cn.shape == (info["bvh_nodes"], 16)
     np.testing.assert_array_equal(cr, nodes[:, 6, :].view(np.int32))
-    org = cn[:, 0:3].view(np.float32)
-    meta = cn[:, 3]
     live = ~((nodes[:, 0, :] == EMPTY) & (nodes[:, 1, :] == EMPTY))  # (n, 4)
-    assert (meta == 0).all()  # reserved
+    assert (cn[:, 3] == 0).all()  # reserved
+    v0 = tris["v0"][:, :3].astype(np.float64)
+    v = np.concatenate([v0, v0 + tris["e1"][:, :3].astype(np.float64), v0 + tris["e2"][:, :3].astype(np.float64)])
+    coords = nodes[:, :6, :].astype(np.float64)[np.broadcast_to(live[:, None, :], (len(nodes), 6, 4))]
+    M = max(4.0 * np.abs(v).max(), 2.0 * np.abs(coords).max(), 2.0 ** -60)
+    G = np.ldexp(M, -21)
+    orgs = cn[:, 0:3].view(np.float32)
+    org = orgs.astype(np.float64) * np.float64(step)  # exact
 
     def codes(words):  # (n, 2) words -> (n, 4) half bit patterns, children 0..3
         return np.stack([words[:, 0] & 0xFFFF, words[:, 0] >> 16, words[:, 1] & 0xFFFF, words[:, 1] >> 16], 1)
 
-    def dec(h, o):  # (+inf codes of empty slots and the NaN patterns above them decode to inf / NaN)
+    def dec(h, o):  # the plane org' + h*s, exact in float64 (+inf codes: inf)
         with np.errstate(invalid="ignore", over="ignore"):
-            return h.astype(np.uint16).view(np.float16).astype(f32) * step + o[:, None]
+            return h.astype(np.uint16).view(np.float16).astype(np.float64) * np.float64(step) + o[:, None]
 
     for a in range(3):
         lo_h, hi_h = codes(cn[:, 4 + 4 * a:6 + 4 * a]), codes(cn[:, 6 + 4 * a:8 + 4 * a])
         # live: finite, non-negative halves; empty: +inf
         assert (lo_h[live] <= 0x7BFF).all() and (hi_h[live] <= 0x7BFF).all()
         assert (lo_h[~live] == 0x7C00).all() and (hi_h[~live] == 0x7C00).all()
-        blo, bhi = nodes[:, 2 * a, :], nodes[:, 2 * a + 1, :]
+        blo = nodes[:, 2 * a, :].astype(np.float64) - G
+        bhi = nodes[:, 2 * a + 1, :].astype(np.float64) + G
         dlo, dhi = dec(lo_h, org[:, a]), dec(hi_h, org[:, a])
         assert (dlo[live] <= blo[live]).all() and (dhi[live] >= bhi[live]).all()
-        # tightest: the next code outward would no longer contain the bound
+        # tightest: the next code outward would no longer keep the margin
         up = live & (lo_h < 0x7BFF)
         assert (dec(lo_h + 1, org[:, a])[up] > blo[up]).all()
         down = live & (hi_h > 0)
         assert (dec(hi_h - 1, org[:, a])[down] < bhi[down]).all()
-        # org = the union's lower bound
-        np.testing.assert_array_equal(org[:, a], np.where(live, blo, np.inf).min(1))
+        # org' <= the union's lower bound - G, and the next float of org/s would exceed it
+        target = np.where(live, blo, np.inf).min(1)
+        assert (org[:, a] <= target).all()
+        nxt = np.nextafter(orgs[:, a], np.float32(np.inf)).astype(np.float64) * np.float64(step)
+        assert (nxt > target).all()
     return info
 
 

@@ -70,9 +70,13 @@ def test_scaled_cornell_vs_oracle(ctx, wgt, oracle, log2s):
     check_counters(g["stats"], r["counters"], oracle)
 
 
+@pytest.mark.parametrize("cnode", ["2", "1"])
 @pytest.mark.parametrize("log2s", [-60, -8, 20])
-def test_scaled_mesh_vs_oracle(ctx, wgt, oracle, log2s):
-    """The BVH path (a 2k-triangle mesh in the Cornell walls) at the same scales."""
+def test_scaled_mesh_vs_oracle(ctx, wgt, oracle, log2s, cnode, monkeypatch):
+    """The BVH path (a 2k-triangle mesh in the Cornell walls) at the same scales, on the
+    auto node form (128-B nodes for this small tree) and forced onto the compact nodes,
+    whose fused slab step relies on the builder's code margin."""
+    monkeypatch.setenv("WGT_CNODE", cnode)
     s = 2.0 ** log2s
     L, Q, S, T = scale_scene(wgt, s, wgt.procedural_mesh("bunny", 2000))
     ctx.upload_scene(L, Q, S, T)
@@ -166,3 +170,39 @@ def test_upload_waits_for_async_render_on_caller_stream(ctx, wgt, oracle):
     stream.synchronize()
     r = oracle.OracleScene(L, Q[:5], S, T).render(oracle.camera_param(W / H, spp, seed), W, H)
     assert_radiance(out.cpu().numpy(), r["f32"])
+
+
+@pytest.mark.parametrize("offset,cam_z", [((65536.0, -32768.0, 16384.0), None), ((0.0, 0.0, 0.0), -1.0e6)])
+def test_compact_nodes_far_origins_vs_oracle(ctx, wgt, oracle, offset, cam_z, monkeypatch):
+    """Compact nodes forced (WGT_CNODE=1) where their code margin matters most:
+    (1) scene and camera translated far from the origin (coordinates ~2^16 against a
+    box of 555: the fused slab step's rounding grows with |org| and |ray origin|, and
+    the margin with them); (2) a camera 10^6 away, beyond the bound the codes were
+    built for, which makes the frame read the 128-B nodes instead.  Bit parity with
+    the oracle either way."""
+    monkeypatch.setenv("WGT_CNODE", "1")
+    L, Q, S, T = wgt.mesh_scene("bunny", target_tris=2000)
+    off = np.array(offset, np.float32)
+    L, Q, S, T = L.copy(), Q.copy(), S.copy(), T.copy()
+    for arr in (L, Q):  # translated quads: the plane offset D = dot(normal, Q) follows (quad.cpp)
+        arr["pos"][:, :3] += off
+        n, p = arr["norm"][:, :3], arr["pos"][:, :3]
+        arr["d"] = (n[:, 0] * p[:, 0] + n[:, 1] * p[:, 1]) + n[:, 2] * p[:, 2]
+    S["center"][:, :3] += off
+    T["v0"][:, :3] += off
+    ctx.upload_scene(L, Q, S, T)
+    W, H, spp, seed = 48, 27, 4, 6
+
+    def cam(mod):
+        c = mod.camera_param(16 / 9, spp, seed)
+        c["origin"] += off
+        c["target"] += off
+        if cam_z is not None:
+            c["origin"][..., 2] = np.float32(cam_z)
+        return c
+
+    g = ctx.render_tile(cam(wgt), W, H, stats=True)
+    r = oracle.OracleScene(L, Q, S, T).render(cam(oracle), W, H)
+    assert_radiance(g["f32"], r["f32"])
+    assert np.array_equal(g["hit"], r["hit"])
+    check_counters(g["stats"], r["counters"], oracle)

@@ -56,6 +56,14 @@ def test_c5_frames_at_size_vs_oracle(ctx, wgt, oracle, bunny_full):
             assert np.array_equal(imgs[f][y0:y0 + 8, x0:x0 + 8], r["u8"]), (f, x0, y0)
         single = ctx.render_tile(wgt.camera_param(W / H, spp, f), W, H, want=("u8",))["u8"]
         assert np.array_equal(imgs[f], single), f
+    # the launcher's pipelined path (frames.py main): batches [1], [0, 1] and [0] on the two
+    # pipeline streams, each frame equal to the batched render
+    seen = []
+    for b, got in FrameRenderer(ctx, W, H, spp).stream([[1], [0, 1], [0]]):
+        for f in b:
+            assert np.array_equal(got[f], imgs[f]), (b, f)
+            seen.append(f)
+    assert seen == [1, 0, 1, 0]
 
 
 @pytest.mark.parametrize("scene", ["cornell", "mesh2k"])

@@ -491,35 +491,46 @@ class DpCollapser {
   std::vector<double> area_;
 };
 
-// Compact form of one node (wgt_geom.h): lo codes are the largest binary16
-// value (bit patterns of non-negative halves order like their values) whose
-// decoded plane is <= the exact bound, hi codes the smallest whose plane is >= it.
-float CDec(uint32_t h, float s, float org) { return qdec(half_bits_to_float(h), s, org); }
-void CompactNode(const float* n, float s, uint32_t* q) {
-  const uint32_t meta = 0;  // reserved
+// Compact form of one node (wgt_geom.h).  The kernel evaluates a child plane's slab
+// distance as fma(h, s/d, c) with c = fma(org/s, s/d, ot) per node and axis (one
+// fused step instead of decoding the plane first), so the codes keep a margin G
+// from the exact child bounds: a lo code's plane org' + h*s (org' = the stored
+// org/s times s) lies <= lo - G, a hi code's >= hi + G.  G = 2^-21 * M, with M
+// >= |org'| and >= |ray origin| (BuildBvh's origin_bound), covers the rounding of
+// c: every decoded interval then contains, bit for bit, the
+// slab interval fma(b, 1/d, ot) of every triangle box b below the child.  Codes
+// are the tightest binary16 values with the margin (non-negative half bit
+// patterns order like their values, so a binary search finds them).
+double CDecD(uint32_t h, double s, double orgd) { return orgd + (double)half_bits_to_float(h) * s; }
+void CompactNode(const float* n, float s, double G, uint32_t* q) {
   bool live[kBvhWidth];
   for (int i = 0; i < kBvhWidth; ++i) live[i] = !(n[i] == kEmptySlotCoord && n[4 + i] == kEmptySlotCoord);
-  float org[3];
+  float orgs[3];
   for (int a = 0; a < 3; ++a) {
-    float ulo = std::numeric_limits<float>::infinity();
+    double ulo = std::numeric_limits<double>::infinity();
     for (int i = 0; i < kBvhWidth; ++i)
-      if (live[i]) ulo = std::min(ulo, n[(2 * a) * 4 + i]);
-    org[a] = ulo;
+      if (live[i]) ulo = std::min(ulo, (double)n[(2 * a) * 4 + i]);
+    // org/s as a float whose value times s is <= ulo - G
+    const double target = (ulo - G) / (double)s;
+    float f = (float)target;
+    while ((double)f > target) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
+    orgs[a] = f;
+    const double orgd = (double)f * (double)s;
     uint32_t lo_h[kBvhWidth], hi_h[kBvhWidth];
     for (int i = 0; i < kBvhWidth; ++i) {
       lo_h[i] = hi_h[i] = 0x7c00u;  // an empty slot: +inf planes on every axis, never entered
       if (!live[i]) continue;
-      const float blo = n[(2 * a) * 4 + i], bhi = n[(2 * a + 1) * 4 + i];
-      uint32_t l = 0, r = 0x7bffu;  // largest h with CDec(h) <= blo (CDec(0) = ulo <= blo)
+      const double blo = (double)n[(2 * a) * 4 + i] - G, bhi = (double)n[(2 * a + 1) * 4 + i] + G;
+      uint32_t l = 0, r = 0x7bffu;  // largest h with plane <= blo (h = 0 is: orgd <= ulo - G)
       while (l < r) {
         const uint32_t m = (l + r + 1) / 2;
-        if (CDec(m, s, ulo) <= blo) l = m; else r = m - 1;
+        if (CDecD(m, s, orgd) <= blo) l = m; else r = m - 1;
       }
       lo_h[i] = l;
-      l = 0; r = 0x7bffu;  // smallest h with CDec(h) >= bhi (the step guarantees h = 65504 does)
+      l = 0; r = 0x7bffu;  // smallest h with plane >= bhi (CompactStep guarantees h = 65504 is)
       while (l < r) {
         const uint32_t m = (l + r) / 2;
-        if (CDec(m, s, ulo) >= bhi) r = m; else l = m + 1;
+        if (CDecD(m, s, orgd) >= bhi) r = m; else l = m + 1;
       }
       hi_h[i] = l;
     }
@@ -528,12 +539,14 @@ void CompactNode(const float* n, float s, uint32_t* q) {
     q[4 + 4 * a + 2] = hi_h[0] | (hi_h[1] << 16);
     q[4 + 4 * a + 3] = hi_h[2] | (hi_h[3] << 16);
   }
-  std::memcpy(&q[0], org, 12);
-  q[3] = meta;
+  std::memcpy(&q[0], orgs, 12);
+  q[3] = 0u;  // reserved
 }
 
-// The smallest power-of-two step with which code 65504 reaches every node's upper bounds.
-float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes) {
+// The smallest power-of-two step with which code 65504 reaches every node's upper
+// bounds plus the margins (the origin sits up to G + one float step of org/s below
+// the lower bound).
+float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes, double G) {
   int e = -24;
   for (;;) {
     const float s = std::ldexp(1.0f, e);
@@ -541,13 +554,14 @@ float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes) {
     for (uint32_t k = 0; k < n_nodes && ok; ++k) {
       const float* n = &nodes[(size_t)k * kNode4Floats];
       for (int a = 0; a < 3 && ok; ++a) {
-        float ulo = std::numeric_limits<float>::infinity(), uhi = -ulo;
+        double ulo = std::numeric_limits<double>::infinity(), uhi = -ulo;
         for (int i = 0; i < kBvhWidth; ++i)
           if (!(n[i] == kEmptySlotCoord && n[4 + i] == kEmptySlotCoord)) {
-            ulo = std::min(ulo, n[(2 * a) * 4 + i]);
-            uhi = std::max(uhi, n[(2 * a + 1) * 4 + i]);
+            ulo = std::min(ulo, (double)n[(2 * a) * 4 + i]);
+            uhi = std::max(uhi, (double)n[(2 * a + 1) * 4 + i]);
           }
-        ok = qdec(65504.0f, s, ulo) >= uhi;
+        const double org_low = ulo - G - (std::fabs(ulo - G) * 0x1p-23 + (double)s * 0x1p-126);
+        ok = org_low + 65504.0 * (double)s >= uhi + G;
       }
     }
     if (ok) return s;
@@ -558,7 +572,7 @@ float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes) {
 }  // namespace
 
 bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
-              uint32_t narrow_limit, double narrow_ratio, BvhOut& out, std::string& err) {
+              uint32_t narrow_limit, double narrow_ratio, double origin_bound, BvhOut& out, std::string& err) {
   out = BvhOut{};
   if (n == 0) { err = "BuildBvh: no triangles"; return false; }
   if (n >= (1u << 28)) { err = "BuildBvh: too many triangles (max 2^28-1)"; return false; }
@@ -662,11 +676,21 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
       }
     }
   }
-  out.cstep = CompactStep(out.nodes, out.n_nodes);
+  // the compact codes' margin: M bounds |ray origin| (the caller's origin_bound) and
+  // every coordinate of the tree (so |org'| <= M as well)
+  double M = std::max(origin_bound, 0x1p-60);
+  for (uint32_t i = 0; i < out.n_nodes; ++i)
+    for (int k = 0; k < 24; ++k) {
+      const float v = out.nodes[(size_t)i * kNode4Floats + k];
+      if (v != kEmptySlotCoord) M = std::max(M, 2.0 * std::fabs((double)v));
+    }
+  out.cbound = (float)M;
+  const double G = std::ldexp(M, -21);
+  out.cstep = CompactStep(out.nodes, out.n_nodes, G);
   out.cnodes.resize((size_t)out.n_nodes * kCNodeFloats);
   out.crefs.resize((size_t)out.n_nodes * 4);
   for (uint32_t i = 0; i < out.n_nodes; ++i) {
-    CompactNode(&out.nodes[(size_t)i * kNode4Floats], out.cstep, &out.cnodes[(size_t)i * kCNodeFloats]);
+    CompactNode(&out.nodes[(size_t)i * kNode4Floats], out.cstep, G, &out.cnodes[(size_t)i * kCNodeFloats]);
     std::memcpy(&out.crefs[(size_t)i * 4], &out.nodes[(size_t)i * kNode4Floats + 24], 16);
   }
   out.tris.resize((size_t)n * kTriRecordFloats);

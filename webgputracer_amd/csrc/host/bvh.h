@@ -16,6 +16,7 @@ struct BvhOut {
   std::vector<uint32_t> cnodes;  // kCNodeFloats words per node: the compact form (wgt_geom.h)
   std::vector<int32_t> crefs;    // 4 child refs per node (the compact form's ref records)
   float cstep = 1.0f;            // scene-wide decode step of the compact nodes
+  float cbound = 0.0f;           // M: the compact codes are exact for ray origins with |o| <= M
   std::vector<float> tris;    // kTriRecordFloats per triangle, leaf order (wgt_geom.h)
   std::vector<float> tshade;  // 8 floats per original triangle
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;  // BVH4 nodes / depth
@@ -31,8 +32,12 @@ struct BvhOut {
 // two-levels-per-node (stack_need <= 3 * ceil(depth2 / 2)).
 // narrow_limit > 0: the BVH2 is also collapsed under that smaller stack bound, and
 // that tree is kept (out.narrow) if it has at most narrow_ratio times the nodes.
+// origin_bound: an upper bound on |coordinate| of every ray origin the compact nodes
+// will see (camera and hit points); the margin of their codes grows with it
+// (CompactNode), and a frame whose camera lies beyond out.cbound reads the 128-B
+// nodes instead.
 constexpr double kNarrowNodeRatio = 1.03;
 bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
-              uint32_t narrow_limit, double narrow_ratio, BvhOut& out, std::string& err);
+              uint32_t narrow_limit, double narrow_ratio, double origin_bound, BvhOut& out, std::string& err);
 
 }  // namespace wgt

@@ -161,9 +161,14 @@ struct Trav {
 // A triangle was accepted (bi starts at kNoHit, see trav_init).
 __device__ __forceinline__ bool trav_found(const Trav& t) { return t.bi != kNoHit; }
 
-__device__ __forceinline__ void trav_init(f3 o, f3 d, bool quad_hit, float qt, Trav& t) {
+// CN (compact nodes): t.inv holds s/d (s = sc.cstep, a power of two: exact), the
+// factor of the fused slab step (cchild_key); the triangle box check multiplies
+// it back by 1/s.
+template <bool CN = false>
+__device__ __forceinline__ void trav_init(const DevScene& sc, f3 o, f3 d, bool quad_hit, float qt, Trav& t) {
   t.inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
   t.ot = slab_offset(o, t.inv);
+  if (CN) t.inv = sc.cstep * t.inv;
   // a triangle must satisfy t < t_quad to beat a quad hit (ray_dist is monotone in
   // t): with bi = kNoHit the rule "t < bt, or t == bt and index < bi" accepts
   // exactly t <= bt, so bt = the float below t_quad (t_quad > 0).  A box entered
@@ -201,18 +206,21 @@ __device__ __forceinline__ float hcode(uint32_t w, uint32_t slot) {
 }
 // Compact node: per axis the ray's entry plane is the lo code for inv >= 0 and the
 // hi code for inv < 0 (one select per two children), which equals the min / max
-// form of child_key because the slab formula is monotone in the plane.  The
-// decode fma(h, s, org) takes h from a half word (v_fma_mix_f32).  An empty slot's
-// +inf codes give n = +inf or f = -inf: a miss without a mask (wgt_geom.h).
-__device__ __forceinline__ uint32_t cchild_key(const Trav& t, const uint32_t* nw, const uint32_t* fw, f3 org,
-                                               float s, uint32_t slot) {
+// form of child_key because the slab formula is monotone in the plane.  The slab
+// distance of the plane org' + h*s is one fused step fma(h, s/d, c) with h taken
+// from a half word (v_fma_mix_f32) and c = fma(org/s, s/d, ot) per node and axis;
+// the builder's code margin makes the interval contain the exact one (wgt_geom.h,
+// DESIGN.md §3.4).  An empty slot's +inf codes give n = +inf or f = -inf: a miss
+// without a mask.
+__device__ __forceinline__ uint32_t cchild_key(const Trav& t, const uint32_t* nw, const uint32_t* fw, f3 c,
+                                               uint32_t slot) {
   const uint32_t k = slot >> 1;
-  const float tnx = __builtin_fmaf(qdec(hcode(nw[0 + k], slot), s, org.x), t.inv.x, t.ot.x);
-  const float tfx = __builtin_fmaf(qdec(hcode(fw[0 + k], slot), s, org.x), t.inv.x, t.ot.x);
-  const float tny = __builtin_fmaf(qdec(hcode(nw[2 + k], slot), s, org.y), t.inv.y, t.ot.y);
-  const float tfy = __builtin_fmaf(qdec(hcode(fw[2 + k], slot), s, org.y), t.inv.y, t.ot.y);
-  const float tnz = __builtin_fmaf(qdec(hcode(nw[4 + k], slot), s, org.z), t.inv.z, t.ot.z);
-  const float tfz = __builtin_fmaf(qdec(hcode(fw[4 + k], slot), s, org.z), t.inv.z, t.ot.z);
+  const float tnx = __builtin_fmaf(hcode(nw[0 + k], slot), t.inv.x, c.x);
+  const float tfx = __builtin_fmaf(hcode(fw[0 + k], slot), t.inv.x, c.x);
+  const float tny = __builtin_fmaf(hcode(nw[2 + k], slot), t.inv.y, c.y);
+  const float tfy = __builtin_fmaf(hcode(fw[2 + k], slot), t.inv.y, c.y);
+  const float tnz = __builtin_fmaf(hcode(nw[4 + k], slot), t.inv.z, c.z);
+  const float tfz = __builtin_fmaf(hcode(fw[4 + k], slot), t.inv.z, c.z);
   const float n = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, kRayMin));
   const float f = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, t.bt));
   return n <= f ? __float_as_uint(n) : kMissKey;
@@ -226,17 +234,19 @@ __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int
     const float4 a = n[0];
     const uint4 x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]),
                 z = __builtin_bit_cast(uint4, n[3]);
-    const f3 org = f3{a.x, a.y, a.z};
+    // c = the slab distance of the node origin org' = (org/s) * s: fma(org/s, s/d, ot)
+    const f3 c = f3{__builtin_fmaf(a.x, t.inv.x, t.ot.x), __builtin_fmaf(a.y, t.inv.y, t.ot.y),
+                    __builtin_fmaf(a.z, t.inv.z, t.ot.z)};
     const bool sx = t.inv.x < 0.0f, sy = t.inv.y < 0.0f, sz = t.inv.z < 0.0f;
     const uint32_t nw[6] = {sx ? x.z : x.x, sx ? x.w : x.y, sy ? y.z : y.x,
                             sy ? y.w : y.y, sz ? z.z : z.x, sz ? z.w : z.y};
     const uint32_t fw[6] = {sx ? x.x : x.z, sx ? x.y : x.w, sy ? y.x : y.z,
                             sy ? y.y : y.w, sz ? z.x : z.z, sz ? z.y : z.w};
     r0 = rf.x, r1 = rf.y, r2 = rf.z, r3 = rf.w;
-    k0 = cchild_key(t, nw, fw, org, sc.cstep, 0u);
-    k1 = cchild_key(t, nw, fw, org, sc.cstep, 1u);
-    k2 = cchild_key(t, nw, fw, org, sc.cstep, 2u);
-    k3 = cchild_key(t, nw, fw, org, sc.cstep, 3u);
+    k0 = cchild_key(t, nw, fw, c, 0u);
+    k1 = cchild_key(t, nw, fw, c, 1u);
+    k2 = cchild_key(t, nw, fw, c, 2u);
+    k3 = cchild_key(t, nw, fw, c, 3u);
   } else {
     const float4* __restrict__ n = sc.nodes + 8 * ref;
     const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
@@ -394,7 +404,7 @@ __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, int* __re
 
 // Test the next triangle of the pending leaf; a lane without a node to visit
 // takes the next stack entry once its leaf is done.
-template <bool STATS>
+template <bool STATS, bool CN = false>
 __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, int* __restrict__ lds,
                                          TravStats& st) {
   const float4* __restrict__ tp = sc.tris + 4 * t.lf;
@@ -406,7 +416,8 @@ __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t
     if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
       const float4 D = tp[3];
       float bn, bf;
-      slab(t.ot, t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
+      // 1/d: under CN t.inv holds s/d, and (s/d) * (1/s) is 1/d exactly
+      slab(t.ot, CN ? sc.rcstep * t.inv : t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
       if (bn <= tt && tt <= bf) {
         t.bt = tt;
         t.bi = idx;
@@ -452,7 +463,7 @@ __device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* 
   float qt;
   quad_scan<EXACT>(sc, o, d, h, qt);
   Trav t;
-  trav_init(o, d, h.prim != kNoHit, qt, t);
+  trav_init(sc, o, d, h.prim != kNoHit, qt, t);
   if (TRIS) {
     while (!trav_step<STATS>(sc, o, d, t, lds, st)) {
     }

@@ -43,7 +43,9 @@ struct DevScene {
   const float4* __restrict__ tris;
   const float4* __restrict__ tshade;
   const float4* __restrict__ cnodes;  // the same tree as 80-B compact records (wgt_geom.h)
-  float cstep;                        // scene-wide decode step of the compact nodes
+  float cstep;                        // scene-wide decode step of the compact nodes (a power of two)
+  float rcstep;                       // 1 / cstep
+  float cbound;                       // the compact codes hold for ray origins with |coordinate| <= cbound
   uint32_t n_lights, n_quads, n_spheres, n_tris;
   uint32_t n_nodes;
   uint32_t last_sphere_emissive;

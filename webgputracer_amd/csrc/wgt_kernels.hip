@@ -232,7 +232,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           }
           Hit h;
           WGT_REGION(cr_quads, quad_scan(sc, ro, rd, h, q_t); q_prim = h.prim;
-                     trav_init(ro, rd, q_prim != kNoHit, q_t, t));
+                     trav_init<CN>(sc, ro, rd, q_prim != kNoHit, q_t, t));
           if (COST) work += fr.pq_svc_cost;
           // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
@@ -272,7 +272,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       if (STATS && (tri_mode ? can_tri : can_node)) simt_count(st.wave_steps, st.lane_steps);
       if (COST && (tri_mode ? can_tri : can_node)) ++work;
       if (tri_mode) {
-        if (can_tri) tri_step<STATS>(sc, ro, rd, t, lds, st);
+        if (can_tri) tri_step<STATS, CN>(sc, ro, rd, t, lds, st);
       } else {
         if (can_node) node_step<STATS, CN>(sc, t, lds, st);
       }
@@ -428,7 +428,11 @@ void ps_launch(const DevScene& sc, bool cn, dim3 grid, dim3 block, size_t lds, h
   }
 }
 
+// The compact codes are exact for ray origins within sc.cbound (their margin, wgt_geom.h):
+// hit points always are, the camera is checked per frame (beyond: the 128-B nodes).
 bool use_compact_nodes(const DevScene& sc, const DevFrame& fr) {
+  const float cam = fmaxf(fmaxf(fabsf(fr.ox), fabsf(fr.oy)), fabsf(fr.oz));
+  if (!(cam <= sc.cbound)) return false;
   return fr.cnode == 1 || (fr.cnode == 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes);
 }
 

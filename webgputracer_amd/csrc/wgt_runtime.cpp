@@ -232,6 +232,29 @@ std::string check_scene_limits(const wgt_quad* lq, uint32_t nlq, const wgt_spher
 
 double sq(double x) { return x * x; }
 
+// Largest |coordinate| any point of the scene's primitives can have (quad corners,
+// sphere boxes, triangle vertices): hit points, i.e. secondary ray origins, lie
+// within it.  The compact nodes are built for ray origins within 4x this bound,
+// which holds the reference camera outside its Cornell box (BuildBvh origin_bound).
+double scene_extent(const wgt_quad* lq, uint32_t nlq, const wgt_sphere* sp, uint32_t ns, const wgt_triangle* tr,
+                    uint32_t nt) {
+  double m = 0.0;
+  for (uint32_t i = 0; i < nlq; ++i)
+    for (int c = 0; c < 3; ++c) {
+      const double p = lq[i].pos[c], r = lq[i].right[c], u = lq[i].up[c];
+      m = std::max({m, std::fabs(p), std::fabs(p + r), std::fabs(p + u), std::fabs(p + r + u)});
+    }
+  for (uint32_t i = 0; i < ns; ++i)
+    for (int c = 0; c < 3; ++c) m = std::max(m, std::fabs((double)sp[i].center[c]) + std::fabs((double)sp[i].radius));
+  for (uint32_t i = 0; i < nt; ++i)
+    for (int c = 0; c < 3; ++c) {
+      const double v = tr[i].v0[c];
+      m = std::max({m, std::fabs(v), std::fabs(v + tr[i].e1[c]), std::fabs(v + tr[i].e2[c])});
+    }
+  return m;
+}
+constexpr double kOriginBoundScale = 4.0;
+
 int check_render_args(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint32_t H,
                       uint32_t tw, uint32_t th) {
   if (!ctx) return fail(nullptr, WGT_E_INVALID, "null context");
@@ -497,7 +520,8 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   if (!tris || n_tris == 0 || !info) return fail(nullptr, WGT_E_INVALID, "null triangles or info");
   BvhOut bvh;
   std::string err;
-  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(), bvh, err))
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(),
+                kOriginBoundScale * scene_extent(nullptr, 0, nullptr, 0, tris, n_tris), bvh, err))
     return fail(nullptr, WGT_E_INVALID, err);
   *info = wgt_scene_info{};
   info->n_tris = n_tris;
@@ -528,7 +552,8 @@ int wgt_bvh_build_compact(const wgt_triangle* tris, uint32_t n_tris, uint32_t* c
     return fail(nullptr, WGT_E_INVALID, "null triangles or outputs");
   BvhOut bvh;
   std::string err;
-  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(), bvh, err))
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(),
+                kOriginBoundScale * scene_extent(nullptr, 0, nullptr, 0, tris, n_tris), bvh, err))
     return fail(nullptr, WGT_E_INVALID, err);
   if (nodes_cap < bvh.n_nodes) return fail(nullptr, WGT_E_INVALID, "node capacity too small");
   std::memcpy(cnodes_out, bvh.cnodes.data(), bvh.cnodes.size() * 4);
@@ -557,7 +582,11 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   BvhOut bvh;
   if (n_tris > 0) {
     std::string err;
-    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(), bvh, err)) return fail(ctx, WGT_E_INVALID, err);
+    const double ext = std::max({scene_extent(lights, n_lights, spheres, n_spheres, tris, n_tris),
+                                 scene_extent(quads, n_quads, nullptr, 0, nullptr, 0)});
+    if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(),
+                  kOriginBoundScale * ext, bvh, err))
+      return fail(ctx, WGT_E_INVALID, err);
   }
   const uint32_t nlq = n_lights + n_quads;
   const size_t b_quads = align256((size_t)nlq * 96);
@@ -609,6 +638,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.tshade = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris);
   sc.cnodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade);
   sc.cstep = bvh.cstep;
+  sc.rcstep = 1.0f / bvh.cstep;  // a power of two: exact
+  sc.cbound = bvh.cbound;
   sc.n_lights = n_lights;
   sc.n_quads = n_quads;
   sc.n_spheres = n_spheres;

@@ -84,7 +84,7 @@ k_wf_init(DevFrame fr, const wgt_tile* __restrict__ tiles, WfState st, uchar4* _
 // The first traversal step on the root decides whether a ray needs the BVH at all.
 __device__ __forceinline__ bool root_needs_trav(const DevScene& sc, f3 o, f3 d, bool quad_hit, float qt) {
   Trav t;
-  trav_init(o, d, quad_hit, qt, t);
+  trav_init(sc, o, d, quad_hit, qt, t);
   uint32_t k0, k1, k2, k3;
   int r0, r1, r2, r3;
   node_keys<false>(sc, t, 0, k0, k1, k2, k3, r0, r1, r2, r3);
@@ -251,7 +251,7 @@ k_wf_trace(DevScene sc, DevFrame fr, WfState st, unsigned long long* __restrict_
           o = ld3(st.ro, st.n, slot);
           d = ld3(st.rd, st.n, slot);
           const uint32_t qp = st.qprim[slot];
-          trav_init(o, d, qp != kNoHit, st.qt[slot], t);
+          trav_init(sc, o, d, qp != kNoHit, st.qt[slot], t);
           active = true;
         }
       }

@@ -12,10 +12,12 @@ The camera is static (Camera::Update ignores t, camera.cpp:64-70), so frames
 differ only by their seed: seed = frame index i (the reference draws
 std::random_device, util.h:43-47; the C++ CLI's --fixed-seed uses the same i).
 
-Frames are rendered B per launch (wgt_render_frames: one full-frame tile per
-frame, each with its frame's seed), so the persistent kernel's end-of-launch
-drain is paid once per B frames instead of once per frame.  Every frame is
-bit-identical to a single-frame render.
+Frames are rendered B per launch (one full-frame tile per frame, each with its
+frame's seed), so the persistent kernel's end-of-launch drain is paid once per B
+frames instead of once per frame, and consecutive launches alternate over the
+context's two pipeline streams (DESIGN.md §4.2a): batch k+1 starts in batch k's
+drain, while the host encodes batch k-1's PNGs.  Every frame is bit-identical to a
+single-frame render.
 
   python -m webgputracer_amd.frames --frame 1 600 --spp 64 --scene bunny --batch 8 --out out/
   python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
@@ -52,8 +54,9 @@ def batches(frames, batch: int):
 
 
 class FrameRenderer:
-    """Renders batches of whole frames on one GPU (wgt_render_frames: one launch per
-    batch, host output)."""
+    """Renders batches of whole frames on one GPU: render() is one synchronous launch
+    per batch (wgt_render_frames); stream() pipelines the batches (a launch per batch
+    on the context's pipeline streams)."""
 
     def __init__(self, ctx: Context, W: int, H: int, spp: int):
         self.ctx, self.W, self.H, self.spp = ctx, W, H, spp
@@ -63,6 +66,52 @@ class FrameRenderer:
         """{frame: (H, W, 4) uint8} for the batch `frames`, seed = frame index."""
         out = self.ctx.render_frames(self.cam, self.W, self.H, np.asarray(frames, np.uint32))
         return {f: out[j] for j, f in enumerate(frames)}
+
+    def stream(self, frame_batches, depth: int = 2):
+        """Yield (batch, {frame: (H, W, 4) uint8}) for each batch of `frame_batches`, in
+        order.  Batch k renders on pipeline stream k % depth into buffer set k % depth;
+        it is issued before batch k-1 is handed out, so the device always has the next
+        launch queued behind the running one.  Host copies are made on the batch's own
+        stream once its launch is done (no pinned buffers: torch's host allocator would
+        outlive the context's streams)."""
+        import torch
+
+        from ._lib import TILE_DTYPE
+
+        dev = torch.device("cuda", self.ctx.device)
+        W, H = self.W, self.H
+        nmax = max((len(b) for b in frame_batches), default=0)
+        if nmax == 0:
+            return
+        streams = [torch.cuda.ExternalStream(self.ctx.pipeline_stream(i), device=dev) for i in range(depth)]
+        d_out = [torch.empty((nmax, H, W, 4), dtype=torch.uint8, device=dev) for _ in range(depth)]
+        pending = []
+        for k, b in enumerate(frame_batches):
+            j = k % depth
+            if len(pending) == depth:  # the oldest batch in flight holds set j: hand it out first
+                yield self._finish(pending.pop(0), streams, d_out)
+            s = streams[j]
+            t = np.zeros(len(b), TILE_DTYPE)  # one full-frame tile per frame (wgt_render_frames' list)
+            t["seed"] = np.asarray(b, np.uint32)
+            t["frame"] = np.arange(len(b), dtype=np.uint32)
+            with torch.cuda.stream(s):
+                d_tiles = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
+                self.ctx.render_tiles_async(self.cam, W, H, W, H, d_tiles.data_ptr(), len(b),
+                                            d_u8=d_out[j].data_ptr(), stream=s.cuda_stream)
+                d_tiles.record_stream(s)
+            pending.append((k, b))
+        while pending:
+            yield self._finish(pending.pop(0), streams, d_out)
+
+    @staticmethod
+    def _finish(kb, streams, d_out):
+        import torch
+
+        k, b = kb
+        j = k % len(streams)
+        with torch.cuda.stream(streams[j]):  # ordered after batch k's launch on its stream
+            imgs = d_out[j][:len(b)].cpu().numpy()
+        return b, {f: imgs[i] for i, f in enumerate(b)}
 
 
 def main(argv=None):
@@ -74,6 +123,7 @@ def main(argv=None):
     ap.add_argument("--scene", default="bunny", help="bunny | sponza | cornell | obj:<path>")
     ap.add_argument("--batch", type=int, default=8,
                     help="frames per launch (8: 30.9 frames/s vs 30.2 at 4, profiles/configs/r01j_c5_frames.jsonl)")
+    ap.add_argument("--pipeline", type=int, default=2, help="batches in flight (1..4, DESIGN.md §4.2a)")
     ap.add_argument("--out", default=None, help="directory for NNN.png (none: render only)")
     a = ap.parse_args(argv)
     if a.frame[0] < 1 or a.frame[1] < a.frame[0]:
@@ -95,13 +145,16 @@ def main(argv=None):
     if a.out:
         os.makedirs(a.out, exist_ok=True)
     t0 = time.perf_counter()
-    for b in batches(mine, a.batch):
-        imgs = fr.render(b)
+    for b, imgs in fr.stream(batches(mine, a.batch), depth=a.pipeline):
         if a.out:
             for f in b:
                 write_png(os.path.join(a.out, f"{f:03d}.png"), imgs[f])  # render.cpp:494-497
     dt = time.perf_counter() - t0
-    print(json.dumps({"rank": rank, "world": world, "frames": len(mine), "batch": a.batch, "seconds": round(dt, 3),
+    import torch
+
+    torch.cuda.synchronize()
+    print(json.dumps({"rank": rank, "world": world, "frames": len(mine), "batch": a.batch, "pipeline": a.pipeline,
+                      "seconds": round(dt, 3),
                       "frames_per_s": round(len(mine) / dt, 3) if dt > 0 else None}), flush=True)
     ctx.close()
 
