@@ -19,9 +19,9 @@ context's two pipeline streams (DESIGN.md §4.2a): batch k+1 starts in batch k's
 drain, while the host encodes batch k-1's PNGs.  Every frame is bit-identical to a
 single-frame render.
 
-  python -m webgputracer_amd.frames --frame 1 600 --spp 64 --scene bunny --batch 8 --out out/
+  python -m webgputracer_amd.frames --frame 1 600 --spp 64 --scene bunny --batch 4 --out out/
   python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
-      -m webgputracer_amd.frames --frame 1 600 --spp 64 --batch 8 --out out/
+      -m webgputracer_amd.frames --frame 1 600 --spp 64 --batch 4 --out out/
 """
 from __future__ import annotations
 
@@ -121,8 +121,9 @@ def main(argv=None):
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--scene", default="bunny", help="bunny | sponza | cornell | obj:<path>")
-    ap.add_argument("--batch", type=int, default=8,
-                    help="frames per launch (8: 30.9 frames/s vs 30.2 at 4, profiles/configs/r01j_c5_frames.jsonl)")
+    ap.add_argument("--batch", type=int, default=4,
+                    help="frames per launch (4 with 2 in flight: 33.0 frames/s, 31.6 at 8, 31.1 at 1; "
+                         "profiles/configs/r02_c5_frames.jsonl)")
     ap.add_argument("--pipeline", type=int, default=2, help="batches in flight (1..4, DESIGN.md §4.2a)")
     ap.add_argument("--out", default=None, help="directory for NNN.png (none: render only)")
     a = ap.parse_args(argv)
