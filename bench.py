@@ -363,9 +363,14 @@ def main():
         if check is not None:
             line["check_frames_bit_exact"] = check
         print(json.dumps(line), flush=True)
-    ctx.close()
+    # teardown: the process group and torch's buffers may still refer to the context's
+    # pipeline streams, so they go first; the context (which destroys its streams) last
+    torch.cuda.synchronize()
     if world > 1:
         dist.destroy_process_group()
+    del shard
+    torch.cuda.set_stream(torch.cuda.default_stream(dev))
+    ctx.close()
 
 
 if __name__ == "__main__":
