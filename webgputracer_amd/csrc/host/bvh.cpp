@@ -575,7 +575,8 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
               uint32_t narrow_limit, double narrow_ratio, double origin_bound, BvhOut& out, std::string& err) {
   out = BvhOut{};
   if (n == 0) { err = "BuildBvh: no triangles"; return false; }
-  if (n >= (1u << 28)) { err = "BuildBvh: too many triangles (max 2^28-1)"; return false; }
+  // leaf walks use 32-bit byte offsets into the 64-B records (wgt_geom.h kTriRecordBytes)
+  if (n >= (1u << 26)) { err = "BuildBvh: too many triangles (max 2^26-1)"; return false; }
   std::vector<Prim> prims(n);
   for (uint32_t i = 0; i < n; ++i) {
     const wgt_triangle& t = tris[i];
@@ -639,6 +640,10 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
     return false;
   }
   out.n_nodes = (uint32_t)(out.nodes.size() / kNode4Floats);
+  if (out.n_nodes >= (1u << 24)) {  // the device copies address nodes by 32-bit byte offsets below kNoRef
+    err = "BuildBvh: too many BVH nodes (max 2^24-1)";
+    return false;
+  }
   if (narrow_limit > 0 && narrow_limit < stack_limit && greedy.Height(0) <= narrow_limit) {
     BvhOut nar;
     if (opt && opt->Cost(narrow_limit) < std::numeric_limits<float>::infinity()) {

@@ -155,7 +155,7 @@ struct Trav {
   float bt;
   uint32_t bi;
   int ref;          // current internal node (when no leaf is open)
-  uint32_t lf, le;  // open leaf: next triangle, end
+  uint32_t lf, le;  // open leaf: byte offsets of the next triangle record and of the leaf's end
   int sp;
 };
 // A triangle was accepted (bi starts at kNoHit, see trav_init).
@@ -229,7 +229,7 @@ template <bool CN>
 __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int ref, uint32_t& k0, uint32_t& k1,
                                           uint32_t& k2, uint32_t& k3, int& r0, int& r1, int& r2, int& r3) {
   if (CN) {
-    const float4* __restrict__ n = sc.cnodes + kCRecordFloat4s * ref;
+    const float4* __restrict__ n = (const float4*)((const char*)sc.cnodes + (uint32_t)ref);  // ref: byte offset
     const int4 rf = __builtin_bit_cast(int4, n[4]);
     const float4 a = n[0];
     const uint4 x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]),
@@ -248,7 +248,7 @@ __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int
     k2 = cchild_key(t, nw, fw, c, 2u);
     k3 = cchild_key(t, nw, fw, c, 3u);
   } else {
-    const float4* __restrict__ n = sc.nodes + 8 * ref;
+    const float4* __restrict__ n = (const float4*)((const char*)sc.nodes + (uint32_t)ref);  // ref: byte offset
     const float4 lx = n[0], hx = n[1], ly = n[2], hy = n[3], lz = n[4], hz = n[5];
     const float4 rf = n[6];
     r0 = __float_as_int(rf.x), r1 = __float_as_int(rf.y), r2 = __float_as_int(rf.z), r3 = __float_as_int(rf.w);
@@ -285,7 +285,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
   bool pop;
   int next = 0;
   if (t.lf < t.le) {
-    const float4* __restrict__ tp = sc.tris + 4 * t.lf;
+    const float4* __restrict__ tp = (const float4*)((const char*)sc.tris + t.lf);
     const float4 A = tp[0], B = tp[1], C = tp[2];
     if (STATS) st.tris++;
     float tt;
@@ -301,7 +301,7 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
         }
       }
     }
-    ++t.lf;
+    t.lf += kTriRecordBytes;
     if (t.lf < t.le) return false;
     pop = true;
   } else {
@@ -331,9 +331,9 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
     next = lds[t.sp * kBlock];
   }
   const bool leaf = next < 0;
-  const uint32_t lfirst = leaf_first(next);
+  const uint32_t lfirst = leaf_first(next) * kTriRecordBytes;
   t.lf = leaf ? lfirst : t.lf;
-  t.le = leaf ? lfirst + leaf_count(next) : t.le;
+  t.le = leaf ? lfirst + leaf_count(next) * kTriRecordBytes : t.le;
   t.ref = leaf ? t.ref : next;
   return false;
 }
@@ -367,8 +367,8 @@ __device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int ca
       return;
     }
     if (t.lf >= t.le) {  // no pending leaf: this one becomes it; keep looking for a node
-      t.lf = leaf_first(cand);
-      t.le = t.lf + leaf_count(cand);
+      t.lf = leaf_first(cand) * kTriRecordBytes;
+      t.le = t.lf + leaf_count(cand) * kTriRecordBytes;
       cand = kNoRef;
       continue;
     }
@@ -407,7 +407,7 @@ __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, int* __re
 template <bool STATS, bool CN = false>
 __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, int* __restrict__ lds,
                                          TravStats& st) {
-  const float4* __restrict__ tp = sc.tris + 4 * t.lf;
+  const float4* __restrict__ tp = (const float4*)((const char*)sc.tris + t.lf);
   const float4 A = tp[0], B = tp[1], C = tp[2];
   if (STATS) st.tris++;
   float tt;
@@ -424,7 +424,7 @@ __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t
       }
     }
   }
-  ++t.lf;
+  t.lf += kTriRecordBytes;
   if (t.lf >= t.le && t.ref == kNoRef) trav_resolve(sc, t, kNoRef, lds);
 }
 

@@ -87,6 +87,7 @@ WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {
 // closest hit, to check t against the triangle's own padded box (tri_box,
 // computed by the host builder with the same fp32 operations).
 constexpr int kTriRecordFloats = 16;
+constexpr uint32_t kTriRecordBytes = kTriRecordFloats * 4;  // the kernels walk a leaf by byte offsets
 
 // BVH4 node, 128 B (8 x float4, one L2 cache line), children in SoA order:
 //   N[0] = lo.x of children 0..3   N[1] = hi.x   N[2] = lo.y   N[3] = hi.y

@@ -600,6 +600,17 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     std::memcpy(&crec[i * kCRecordFloat4s * 4], &bvh.cnodes[i * kCNodeFloats], kCNodeFloats * 4);
     std::memcpy(&crec[i * kCRecordFloat4s * 4 + kCNodeFloats], &bvh.crefs[i * 4], 16);
   }
+  // device copies address child nodes by byte offset (one add to the uniform base in
+  // the kernels instead of an index multiply); leaf refs are unchanged
+  for (size_t i = 0; i < bvh.n_nodes; ++i)
+    for (int k = 0; k < 4; ++k) {
+      int32_t& r = reinterpret_cast<int32_t&>(crec[i * kCRecordFloat4s * 4 + kCNodeFloats + k]);
+      if (r >= 0) r *= (int32_t)(kCRecordFloat4s * 16);
+      int32_t r128;
+      std::memcpy(&r128, &bvh.nodes[i * kNode4Floats + 24 + k], 4);
+      if (r128 >= 0) r128 *= (int32_t)(kNode4Floats * 4);
+      std::memcpy(&bvh.nodes[i * kNode4Floats + 24 + k], &r128, 4);
+    }
   const size_t b_cnodes = align256(crec.size() * 4);
   const size_t b_tris = align256(bvh.tris.size() * 4);
   const size_t b_shade = align256(bvh.tshade.size() * 4);
