@@ -122,7 +122,13 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   int depth = 0;
   TravStats st{0u, 0u, 0u, 0u};
   Counters c{0u, 0u, 0u, 0u, 0u, 0u};
+  // invariant: trav == !trav_done(t) (a lane leaves the traversal exactly when
+  // trav_done turns true), so a lane with a node to visit or a pending leaf is
+  // traversing; a lane starts done
   Trav t;
+  t.ref = kNoRef;
+  t.lf = t.le = 0u;
+  t.sp = 0;
   uint32_t q_prim = kNoHit;  // quad part of the pending hit, rebuilt at finalisation
   float q_t = kRayMax;
   bool have = false;       // lane holds a pixel
@@ -264,8 +270,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
     for (; TRIS;) {
       // one uniform mode per step: triangle steps once enough lanes hold a
       // pending leaf (weighted by the two steps' costs), else node steps
-      const bool can_node = trav && t.ref != kNoRef;
-      const bool can_tri = trav && t.lf < t.le;
+      const bool can_node = t.ref != kNoRef;  // implies trav (invariant above)
+      const bool can_tri = t.lf < t.le;       // implies trav
       const uint32_t nn = (uint32_t)__popcll(__ballot(can_node));
       const uint32_t nl = (uint32_t)__popcll(__ballot(can_tri));
       const bool tri_mode = nn == 0 || nl * 100u >= nn * fr.tri_ratio;
