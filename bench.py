@@ -41,13 +41,13 @@ METRIC = "Mrays/sec at 1080p/256spp + achieved HBM GB/s vs peak, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # algorithmic bytes per unit: a BVH4 node visit reads 7 x 16 B (6 SoA
 # box rows + child refs) of its 128-B line, or with compact nodes 4 x 16 B of its
-# 64-B node + its 16-B ref record; a triangle test 3 x 16 B of its 64-B record (the
-# 4th, the padded box, only for a candidate closest hit), a traced ray 32 B of
-# per-triangle shading data
-NODE_BYTES, CNODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 48, 32
+# 64-B node + its 16-B ref record; a triangle test all 4 x 16 B of its 64-B record
+# (the padded box with the Moller-Trumbore inputs), a traced
+# ray 32 B of per-triangle shading data
+NODE_BYTES, CNODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 64, 32
 # SURVEY §8(d)'s format-independent figure: 32 B per BVH node visit, 48 B per triangle
 # test, 32 B of shading record per traced ray (the same at any node encoding)
-SURVEY_NODE_BYTES = 32
+SURVEY_NODE_BYTES, SURVEY_TRI_BYTES = 32, 48
 L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the 8 XCDs
 L2_CALIB_JSON = os.path.join(ROOT, "profiles", "l2_calibration.json")
 
@@ -288,7 +288,7 @@ def main():
         node_b = CNODE_BYTES if compact else NODE_BYTES
         bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-        survey_bytes = mine[4] * SURVEY_NODE_BYTES + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES
+        survey_bytes = mine[4] * SURVEY_NODE_BYTES + mine[5] * SURVEY_TRI_BYTES + mine[1] * SHADE_BYTES
         traffic, l2 = None, None
         try:
             with open(args.traffic_json) as f:
@@ -350,7 +350,7 @@ def main():
                                        else 0.0,
                                        "frac": round(survey_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
                                        if kern_ms > 0 else 0.0,
-                                       "bytes_per_unit": {"node": SURVEY_NODE_BYTES, "tri": TRI_BYTES,
+                                       "bytes_per_unit": {"node": SURVEY_NODE_BYTES, "tri": SURVEY_TRI_BYTES,
                                                           "shade_per_ray": SHADE_BYTES}},
                          # L2 request traffic of the timed kernel (PMC pass, calibrated request size)
                          "l2": l2,

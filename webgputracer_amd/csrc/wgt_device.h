@@ -408,13 +408,14 @@ template <bool STATS, bool CN = false>
 __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, int* __restrict__ lds,
                                          TravStats& st) {
   const float4* __restrict__ tp = (const float4*)((const char*)sc.tris + t.lf);
-  const float4 A = tp[0], B = tp[1], C = tp[2];
+  // all four float4 of the record at once: the padded box D (for a candidate
+  // closest hit) used to be loaded in the branch, a second dependent round trip
+  const float4 A = tp[0], B = tp[1], C = tp[2], D = tp[3];
   if (STATS) st.tris++;
   float tt;
   if (mt_test(o, d, xyz(A), xyz(B), xyz(C), tt)) {
     const uint32_t idx = __float_as_uint(A.w);
     if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
-      const float4 D = tp[3];
       float bn, bf;
       // 1/d: under CN t.inv holds s/d, and (s/d) * (1/s) is 1/d exactly
       slab(t.ot, CN ? sc.rcstep * t.inv : t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
