@@ -431,13 +431,22 @@ __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t
 
 // Merge the triangle result into the quad hit, then scan the spheres: the end of
 // sample_hit (path_tracer.wgsl:305-309) with triangles between quads and spheres.
-__device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const Trav& t, Hit& h) {
+// PRELOAD: the triangle's shading record is read before the quad hit is rebuilt (the
+// caller issues both loads together, preload_tshade) instead of after the distance
+// comparison that needs it: one memory round trip per finalise instead of two.
+__device__ __forceinline__ void preload_tshade(const DevScene& sc, const Trav& t, float4& s0, float4& s1) {
+  const uint32_t i = trav_found(t) ? t.bi : 0u;  // record 0 for a ray without a triangle hit: unused
+  s0 = sc.tshade[2 * i];
+  s1 = sc.tshade[2 * i + 1];
+}
+__device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const Trav& t, Hit& h,
+                                           const float4* pre = nullptr) {
   const uint32_t nlq = sc.n_lights + sc.n_quads;
   if (trav_found(t)) {
     const f3 pos = o + t.bt * d;
     const float ray_dist = distance(pos, o);
     if (!(ray_dist >= h.dist)) {
-      const float4 s0 = sc.tshade[2 * t.bi], s1 = sc.tshade[2 * t.bi + 1];
+      const float4 s0 = pre ? pre[0] : sc.tshade[2 * t.bi], s1 = pre ? pre[1] : sc.tshade[2 * t.bi + 1];
       const f3 fn = xyz(s0);
       const bool ff = dot(d, fn) < 0.0f;
       h.dist = ray_dist;

@@ -198,7 +198,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             if (STATS) { ++c.q; ++c.nan; }
             nanray = false;
           } else {
-            WGT_REGION(cr_fin, quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h));
+            WGT_REGION(cr_fin, float4 pre[2]; preload_tshade(sc, t, pre[0], pre[1]);
+                       quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h, pre));
             if (STATS) { ++c.q; ++c.tr; }
           }
           first_hit(px, depth, h.prim, po, outhit);
