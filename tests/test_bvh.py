@@ -220,20 +220,26 @@ def test_compact_nodes_full_size_meshes():
         assert check_compact(tris)["bvh_compact"] == compact
 
 
-def test_narrow_tree_selects_six_waves(monkeypatch):
-    """A tree that collapses under the 25-entry stack bound at <= 3% more SAH cost
-    (greedy collapse: nodes) is kept narrow, and the persistent kernel runs 6 waves
-    per SIMD on it (bunny stand-in: SAH-optimal trees of cost 22.77 at 25 entries vs
-    22.63 at 31); sponza's would cost 5% more, so it keeps the 31-entry bound and 5
-    waves.  WGT_PS_WAVES=5 keeps every tree wide."""
+def test_wave_budget_and_narrow_tree(monkeypatch):
+    """The persistent kernel runs 6 waves per SIMD with 3-byte stack entries whenever
+    every ref of the tree fits them (< 2^16 nodes, < 2^20 triangles): both stand-ins, on
+    their wide trees (the 31-entry bound).  WGT_NARROW=1 builds the 25-entry tree when
+    its SAH cost is within 3% of the wide one's (bunny stand-in: SAH-optimal trees of cost
+    22.77 at 25 entries vs 22.63 at 31; sponza's would cost 5% more and stays wide);
+    WGT_PS_WAVES=5 selects 5 waves with 4-byte entries."""
+    for kind in ("bunny", "sponza"):
+        info, _, _ = w.bvh_build(w.procedural_mesh(kind))
+        assert info["ps_waves"] == 6 and info["bvh_nodes"] < 1 << 16
+        assert 25 < info["bvh_stack"] <= 31
+    monkeypatch.setenv("WGT_NARROW", "1")
     bunny = w.procedural_mesh("bunny", 20000)
     info = check_tree(bunny)  # the exported (= uploaded) tree passes the full walk
     assert info["ps_waves"] == 6 and info["bvh_stack"] <= 25
-    for kind, waves in (("bunny", 6), ("sponza", 5)):
+    for kind, stack in (("bunny", 25), ("sponza", 31)):
         info, _, _ = w.bvh_build(w.procedural_mesh(kind))
-        assert info["ps_waves"] == waves
-        assert info["bvh_stack"] <= (25 if waves == 6 else 31)
+        assert info["ps_waves"] == 6 and info["bvh_stack"] <= stack
     monkeypatch.setenv("WGT_PS_WAVES", "5")
+    monkeypatch.delenv("WGT_NARROW")
     info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
     assert info["ps_waves"] == 5 and info["bvh_stack"] == 31
 

@@ -256,12 +256,12 @@ def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
 def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp):
     """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
     oracle (OpenMP), through the default kernel of each scene: sponza on the compact
-    nodes at 5 waves/SIMD, bunny on the narrow 128-B tree at 6."""
+    nodes, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries."""
     L, Q, S, T = wgt.mesh_scene(kind)
     ctx.upload_scene(L, Q, S, T)
     info = ctx.scene_info()
     if not any(os.environ.get(k) for k in ("WGT_CNODE", "WGT_PS_WAVES", "WGT_STACK_LIMIT")):  # the defaults
-        assert (info["bvh_compact"], info["ps_waves"]) == ((1, 5) if kind == "sponza" else (0, 6))
+        assert (info["bvh_compact"], info["ps_waves"]) == ((1, 6) if kind == "sponza" else (0, 6))
     osc = oracle.OracleScene(L, Q, S, T)
     g = ctx.render_tile(wgt.camera_param(16 / 9, spp, 3), 1920, 1080, stats=True)
     r = osc.render(oracle.camera_param(16 / 9, spp, 3), 1920, 1080)
@@ -311,12 +311,13 @@ _SCHED_REF = {}
                                  {"WGT_PQ_LPT": "2"}, {"WGT_PQ_LPT_ALL": "0"}, {"WGT_PS_SVC_FRAC": "0"},
                                  {"WGT_PS_SVC_FRAC": "1"},
                                  {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
-                                 {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}])
+                                 {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}, {"WGT_NARROW": "1"}])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the
     cost pre-pass (1 or 4 spp) or block order; refill threshold; phase thresholds and
     their sparse-wave scaling; the node form: compact nodes forced on the bunny; the
-    bunny's narrow tree at 6 waves per SIMD or, with WGT_PS_WAVES=5, its wide one at 5)
+    wave budget: 6 waves per SIMD with 3-byte stack entries or, with WGT_PS_WAVES=5, 5
+    with 4-byte ones; the narrow 25-entry tree, WGT_NARROW=1)
     change which lane renders which pixel and when, never a bit of the result.  100x60
     leaves ragged 8x8 blocks at the frame edge.  The test runs after the kernel-family
     tests on the same context, the sequence that exposed a workspace-reuse bug (each

@@ -353,14 +353,36 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
 // pending leaf (lf < le), or done (kNoRef, no pending leaf, empty stack).
 constexpr int kNoRef = 0x7fffffff;
 
+// The per-lane LDS traversal stack of k_render_ps, entry i of a lane at stride
+// kBlock (conflict-free).  Stack32: one int per entry.  Stack24: a 16-bit and an
+// 8-bit array (3 B per entry, the high byte sign-extending), which fits every ref
+// of a tree with fewer than 2^16 nodes and 2^20 triangles (byte offsets < 2^23,
+// leaf refs >= -2^23; DevScene::ps_waves) and lets LDS hold the full 31-entry
+// bound of 24 waves per CU: 6 waves per SIMD without a narrower tree.
+struct Stack32 {
+  int* __restrict__ p;
+  __device__ __forceinline__ int ld(int i) const { return p[i * kBlock]; }
+  __device__ __forceinline__ void st(int i, int v) const { p[i * kBlock] = v; }
+};
+struct Stack24 {
+  uint16_t* __restrict__ lo;
+  int8_t* __restrict__ hi;
+  __device__ __forceinline__ int ld(int i) const { return ((int)hi[i * kBlock] << 16) | (int)lo[i * kBlock]; }
+  __device__ __forceinline__ void st(int i, int v) const {
+    lo[i * kBlock] = (uint16_t)v;
+    hi[i * kBlock] = (int8_t)(v >> 16);
+  }
+};
+
 // Place `cand` (a child ref, or kNoRef = take the next stack entry).
-__device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int cand, int* __restrict__ lds) {
+template <class STK>
+__device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int cand, const STK& lds) {
 #pragma unroll
   for (int it = 0; it < 3; ++it) {
     if (cand == kNoRef) {
       if (t.sp == 0) break;
       --t.sp;
-      cand = lds[t.sp * kBlock];
+      cand = lds.ld(t.sp);
     }
     if (cand >= 0) {
       t.ref = cand;
@@ -372,7 +394,7 @@ __device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int ca
       cand = kNoRef;
       continue;
     }
-    lds[t.sp * kBlock] = cand;  // a second leaf waits on the stack
+    lds.st(t.sp, cand);  // a second leaf waits on the stack
     ++t.sp;
     break;
   }
@@ -382,8 +404,8 @@ __device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int ca
 __device__ __forceinline__ bool trav_done(const Trav& t) { return t.ref == kNoRef && t.lf >= t.le && t.sp == 0; }
 
 // Visit t.ref: sort the hit children, push all but the nearest, place the nearest.
-template <bool STATS, bool CN>
-__device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, int* __restrict__ lds, TravStats& st) {
+template <bool STATS, bool CN, class STK>
+__device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
   if (STATS) st.nodes++;
   uint32_t k0, k1, k2, k3;
   int r0, r1, r2, r3;
@@ -393,19 +415,19 @@ __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, int* __re
   cas(k0, r0, k2, r2);
   cas(k1, r1, k3, r3);
   cas(k1, r1, k2, r2);
-  lds[t.sp * kBlock] = r3;
+  lds.st(t.sp, r3);
   t.sp += k3 != kMissKey ? 1 : 0;
-  lds[t.sp * kBlock] = r2;
+  lds.st(t.sp, r2);
   t.sp += k2 != kMissKey ? 1 : 0;
-  lds[t.sp * kBlock] = r1;
+  lds.st(t.sp, r1);
   t.sp += k1 != kMissKey ? 1 : 0;
   trav_resolve(sc, t, k0 != kMissKey ? r0 : kNoRef, lds);
 }
 
 // Test the next triangle of the pending leaf; a lane without a node to visit
 // takes the next stack entry once its leaf is done.
-template <bool STATS, bool CN = false>
-__device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, int* __restrict__ lds,
+template <bool STATS, bool CN = false, class STK>
+__device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, const STK& lds,
                                          TravStats& st) {
   const float4* __restrict__ tp = (const float4*)((const char*)sc.tris + t.lf);
   // all four float4 of the record at once: the padded box D (for a candidate

@@ -25,9 +25,9 @@ constexpr int kBlock = 64;        // one wave per block: 8x8 pixels
 // cannot overflow and needs no spill path.  kMaxBvhDepth bounds the SAH BVH2 the
 // BVH4 is collapsed from; kStackMax bounds the builder's stack need: + 1 parking
 // slot, so that LDS (160 KB per CU) admits 5 waves per SIMD (4 SIMDs per CU):
-// 32 entries = 8 KB per wave.  A tree that collapses under kStackNarrow at
-// nearly the same size runs k_render_ps at 6 waves per SIMD instead (26 entries =
-// 6.5 KB per wave, 80 VGPRs): DevScene::ps_waves.
+// 32 entries = 8 KB per wave.  k_render_ps stores 3-byte entries when the tree's
+// refs fit them (6 KB per wave): 6 waves per SIMD at 80 VGPRs (DESIGN.md §4.2,
+// DevScene::ps_waves).  kStackNarrow is the optional narrow collapse (WGT_NARROW).
 constexpr int kMaxBvhDepth = 24;
 constexpr int kStackMax = 31;
 constexpr int kStackNarrow = 25;
@@ -35,6 +35,7 @@ constexpr int kStackNarrow = 25;
 constexpr int kPsWavesNoTris = 8;
 static_assert((kStackMax + 1) * kBlock * 4 * 5 * 4 <= 160 * 1024, "5 waves per SIMD");
 static_assert((kStackNarrow + 1) * kBlock * 4 * 6 * 4 <= 160 * 1024, "6 waves per SIMD");
+static_assert((kStackMax + 1) * kBlock * 3 * 6 * 4 <= 160 * 1024, "6 waves per SIMD, 3-byte entries");
 
 struct DevScene {
   const float4* __restrict__ quads;   // n_lights + n_quads records
@@ -51,10 +52,18 @@ struct DevScene {
   uint32_t last_sphere_emissive;
   float light_area;  // length(cross(lights[0].right, lights[0].up)) (path_tracer.wgsl:205)
   uint32_t stack;     // traversal stack entries per lane (>= 1)
-  uint32_t ps_waves;  // k_render_ps waves per SIMD: 6 for a tree built for kStackNarrow, else 5
+  // k_render_ps waves per SIMD: 6 (3-byte stack entries, Stack24) when every ref of
+  // the tree fits 24 bits (kStack24Nodes, kStack24Tris), else 5
+  uint32_t ps_waves;
 };
-// Dynamic LDS bytes of a traversal kernel launch.
+constexpr uint32_t kStack24Nodes = 1u << 16;  // 128-B node byte offsets < 2^23
+constexpr uint32_t kStack24Tris = 1u << 20;   // leaf refs ~(first << 3 | count - 1) >= -2^23
+// Dynamic LDS bytes of a traversal kernel launch (4-byte entries).
 inline size_t stack_lds_bytes(const DevScene& sc) { return (size_t)sc.stack * kBlock * sizeof(int); }
+// ... of a k_render_ps launch: 3-byte entries at 6 waves per SIMD
+inline size_t ps_stack_lds_bytes(const DevScene& sc) {
+  return sc.ps_waves == 6 ? (size_t)sc.stack * kBlock * 3 : stack_lds_bytes(sc);
+}
 
 // 1 / spp when spp is a power of two (exact in fp32: end_sample multiplies), else 0
 inline float pow2_recip(uint32_t spp) { return (spp != 0u && (spp & (spp - 1u)) == 0u) ? 1.0f / (float)spp : 0.0f; }

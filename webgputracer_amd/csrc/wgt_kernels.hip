@@ -30,6 +30,8 @@
 // colour (contributing max(NaN, 0) = 0), so the LCG is advanced by 3*(50-depth)
 // steps in O(8) and the sample ends: bit-identical output, ~2/3 fewer queries on
 // the Cornell box.
+#include <type_traits>
+
 #include "wgt_device.h"
 
 namespace wgt {
@@ -109,8 +111,16 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
             unsigned long long* __restrict__ counters, uint32_t* __restrict__ queue) {
-  extern __shared__ int s_stack[];  // sc.stack entries per lane (stack_lds_bytes)
-  int* lds = s_stack + threadIdx.x;
+  extern __shared__ int s_stack[];  // sc.stack entries per lane (ps_stack_lds_bytes)
+  // 6 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
+  using STK = typename std::conditional<W == 6, Stack24, Stack32>::type;
+  STK lds;
+  if constexpr (W == 6) {
+    lds.lo = (uint16_t*)s_stack + threadIdx.x;
+    lds.hi = (int8_t*)((uint16_t*)s_stack + sc.stack * kBlock) + threadIdx.x;
+  } else {
+    lds.p = s_stack + threadIdx.x;
+  }
   const uint32_t lane = threadIdx.x;
   const unsigned long long lt_mask = (1ull << lane) - 1ull;
   const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
@@ -460,6 +470,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   const size_t lds = stack_lds_bytes(sc);
   const bool tris = sc.n_tris > 0;
   if (fr.kernel == 2) {
+    const size_t plds = ps_stack_lds_bytes(sc);
     if (blocks * 64ull > 0xffffffffull || resident == 0) return hipErrorInvalidValue;
     if (!ws || ws_cap < render_ws_bytes(fr)) return hipErrorInvalidValue;
     const uint32_t nb = (uint32_t)blocks;
@@ -486,14 +497,14 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       fc.inv_fspp = pow2_recip(fc.sqrt_spp * fc.sqrt_spp);
       fc.cost = (uint32_t*)((char*)ws + 256);
       fc.n_slots = nb * (fr.pq_lpt_all ? 64u : 16u);  // by default a quarter of each block's pixels estimate its cost
-      ps_launch<false, true>(sc, cn, grid, block, lds, stream, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
+      ps_launch<false, true>(sc, cn, grid, block, plds, stream, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
       k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb);
       f.perm = fc.cost + nb;
       e = hipGetLastError();
     }
     if (e == hipSuccess) {
-      if (counters) ps_launch<true, false>(sc, cn, grid, block, lds, stream, f, d_tiles, out8, out32, outhit, counters, q + 1);
-      else ps_launch<false, false>(sc, cn, grid, block, lds, stream, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
+      if (counters) ps_launch<true, false>(sc, cn, grid, block, plds, stream, f, d_tiles, out8, out32, outhit, counters, q + 1);
+      else ps_launch<false, false>(sc, cn, grid, block, plds, stream, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
       e = hipGetLastError();
     }
     return e;
@@ -528,7 +539,7 @@ hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
   for (const void* k : variants) {
     if (sc.n_tris == 0) break;
     int n = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, stack_lds_bytes(sc));
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, ps_stack_lds_bytes(sc));
     if (e != hipSuccess) return e;
     per_cu = n > per_cu ? n : per_cu;
   }

@@ -141,10 +141,18 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 // operations as the WGSL per-invocation evaluation.
 // The builder's stack bound (WGT_STACK_LIMIT overrides kStackMax for sweeps).
 uint32_t stack_limit() { return std::min(env_u32("WGT_STACK_LIMIT", (uint32_t)kStackMax), (uint32_t)kStackMax); }
-// The narrow collapse for 6 waves per SIMD: WGT_PS_WAVES=5 keeps every tree at 5,
-// 6 takes the narrow tree whenever the BVH2 is shallow enough (sweeps).
-uint32_t narrow_limit() { return env_u32("WGT_PS_WAVES", 0) == 5 ? 0u : (uint32_t)kStackNarrow; }
-double narrow_ratio() { return env_u32("WGT_PS_WAVES", 0) == 6 ? 1e30 : kNarrowNodeRatio; }
+// The narrow collapse (a 25-entry stack bound), off by default since 3-byte stack
+// entries give 6 waves per SIMD the full bound: WGT_NARROW=1 takes it when its SAH
+// cost is within kNarrowNodeRatio of the wide tree's, 2 whenever the BVH2 is shallow
+// enough (sweeps).
+uint32_t narrow_limit() { return env_u32("WGT_NARROW", 0) ? (uint32_t)kStackNarrow : 0u; }
+double narrow_ratio() { return env_u32("WGT_NARROW", 0) == 2 ? 1e30 : kNarrowNodeRatio; }
+// k_render_ps waves per SIMD (DevScene::ps_waves): 6 with 3-byte stack entries when
+// every ref fits them, else 5; WGT_PS_WAVES=5 forces 5 (sweeps).
+uint32_t ps_waves_for(const BvhOut& bvh, uint32_t n_tris) {
+  if (env_u32("WGT_PS_WAVES", 0) == 5) return 5u;
+  return bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris ? 6u : 5u;
+}
 
 DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   DevFrame fr{};
@@ -542,7 +550,7 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   if (tris_out) std::memcpy(tris_out, bvh.tris.data(), bvh.tris.size() * 4);
   info->bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
   info->bvh_compact_step = bvh.cstep;
-  info->ps_waves = bvh.narrow ? 6u : 5u;
+  info->ps_waves = ps_waves_for(bvh, n_tris);
   return WGT_OK;
 }
 
@@ -662,7 +670,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
   // + 1: the speculative traversal parks a second leaf on the stack (wgt_device.h)
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
-  sc.ps_waves = bvh.narrow ? 6u : 5u;
+  sc.ps_waves = ps_waves_for(bvh, n_tris);
   WGT_HIP(ctx, ps_resident_waves(sc, ctx->device, ctx->ps_resident));
 
   wgt_scene_info& in = ctx->info;
