@@ -403,7 +403,12 @@ __device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int ca
 
 __device__ __forceinline__ bool trav_done(const Trav& t) { return t.ref == kNoRef && t.lf >= t.le && t.sp == 0; }
 
-// Visit t.ref: sort the hit children, push all but the nearest, place the nearest.
+// Visit t.ref: bring the nearest hit child to slot 0 (three compare-exchanges: the
+// pairs, then their minima), push the other three unordered, place the nearest.
+// The full 5-exchange network cost 10 more VALU per node step for 0.6% fewer node
+// visits.  Any order is exact (the closest hit is a minimum
+// over (t, index)), and a missed child's kMissKey keeps it off the stack wherever it
+// sits: each push advances the top only for a hit.
 template <bool STATS, bool CN, class STK>
 __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
   if (STATS) st.nodes++;
@@ -413,8 +418,6 @@ __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, const STK
   cas(k0, r0, k1, r1);
   cas(k2, r2, k3, r3);
   cas(k0, r0, k2, r2);
-  cas(k1, r1, k3, r3);
-  cas(k1, r1, k2, r2);
   lds.st(t.sp, r3);
   t.sp += k3 != kMissKey ? 1 : 0;
   lds.st(t.sp, r2);
