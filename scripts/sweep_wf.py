@@ -13,7 +13,7 @@ import webgputracer_amd as w  # noqa: E402
 scene = sys.argv[1] if len(sys.argv) > 1 else "bunny"
 W, H, spp = (int(v) for v in sys.argv[2:5]) if len(sys.argv) > 4 else (1920, 1080, 64)
 ctx = w.Context(0)
-ctx.upload_scene(*w.mesh_scene(scene))
+ctx.upload_scene(*(w.cornell_scene() if scene == "cornell" else w.mesh_scene(scene)))
 cam = w.camera_param(W / H, spp, 0)
 print(json.dumps(ctx.scene_info()), flush=True)
 ref = None
