@@ -244,6 +244,15 @@ def test_wave_budget_and_narrow_tree(monkeypatch):
     assert info["ps_waves"] == 5 and info["bvh_stack"] == 31
 
 
+def test_stack24_fit_rule():
+    """6 waves per SIMD need every ref in a 3-byte stack entry: a tree of 2^20 triangles (leaf refs
+    below -2^23) and > 2^16 nodes (128-B node offsets >= 2^23) falls back to 5 waves and 4-byte
+    entries (wgt_runtime.cpp ps_waves_for, wgt_internal.h kStack24Nodes / kStack24Tris)."""
+    info, _, _ = w.bvh_build(random_soup(1 << 20, 7))
+    assert info["n_tris"] == 1 << 20 and info["bvh_nodes"] >= 1 << 16
+    assert info["ps_waves"] == 5
+
+
 def bvh4_sah(nodes):
     """SAH cost of an exported BVH4 (root-relative): the root plus every internal child's box
     area (node visits), and count x area of every leaf child (triangle tests)."""
