@@ -484,7 +484,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
     // phase thresholds swept per wave budget (profiles/sweeps/r01_sweep_compact_knobs.jsonl)
     if (f.ps_to_trav == 0) f.ps_to_trav = sc.ps_waves == 6 ? 16u : 18u;
     if (f.ps_to_service == 0) f.ps_to_service = sc.ps_waves == 6 ? 14u : 16u;
-    if (f.pq_refill == 0) f.pq_refill = sc.ps_waves == 6 ? 3u : 2u;
+    if (f.pq_refill == 0) f.pq_refill = 2u;
     f.n_slots = nb * 64u;
     f.perm = nullptr;
     f.cost = nullptr;

@@ -194,7 +194,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
   fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
   fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
-  fr.pq_refill = env_u32("WGT_PQ_REFILL", 0);  // 0 = by waves per SIMD: 2 at 5, 3 at 6 (launch_render)
+  fr.pq_refill = env_u32("WGT_PQ_REFILL", 0);  // 0 = the default, 2 (launch_render)
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   fr.pq_svc_cost = env_u32("WGT_PQ_SVC_COST", 7);
