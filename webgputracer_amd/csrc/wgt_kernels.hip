@@ -6,8 +6,9 @@
 // sample-level parallelism — parallelism is over pixels only.
 //
 // sample_hit (path_tracer.wgsl:290-310) = linear scan of lights and quads (scalar
-// loads: the scene is wave-uniform), BVH2 traversal over triangles (per-lane LDS
-// stack, Moller-Trumbore in fp32, wgt_geom.h), then the sphere scan.
+// loads: the scene is wave-uniform), BVH4 traversal over triangles (per-lane LDS
+// stack of 4-byte entries, or 3-byte ones in k_render_ps at 6 waves per SIMD;
+// Moller-Trumbore in fp32, wgt_geom.h), then the sphere scan.
 //
 // Two kernels compute bit-identical results:
 //  * k_render (simple, WGT_KERNEL=1): a flat per-lane loop, one closest-hit query +
