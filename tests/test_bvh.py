@@ -244,6 +244,31 @@ def test_wave_budget_and_narrow_tree(monkeypatch):
     assert info["ps_waves"] == 5 and info["bvh_stack"] == 31
 
 
+def stack24_roundtrip(v):
+    """Stack24 (wgt_device.h): a ref stored as its low 16 bits and its bits 16..23 as a signed byte,
+    read back as (int8 << 16) | uint16."""
+    v = np.asarray(v, np.int64)
+    lo = (v & 0xFFFF).astype(np.uint16)
+    hi = ((v >> 16) & 0xFF).astype(np.uint8).view(np.int8)
+    return (hi.astype(np.int64) << 16) | lo.astype(np.int64)
+
+
+@pytest.mark.parametrize("kind", ["bunny", "sponza"])
+def test_stack24_holds_every_ref(kind):
+    """Every ref the 6-wave kernel can push survives the 3-byte stack entry: internal refs as the
+    device's byte offsets into either node form (x 128 for 128-B nodes, x 80 for compact records)
+    and leaf refs as they are (wgt_runtime.cpp converts the device copies)."""
+    tris = w.procedural_mesh(kind)
+    info, nodes, _ = w.bvh_build(tris)
+    assert info["ps_waves"] == 6
+    refs = nodes.reshape(-1, 8, 4)[:, 6, :].view(np.int32).ravel().astype(np.int64)
+    for stride in (128, 80):
+        dev = np.where(refs >= 0, refs * stride, refs)
+        assert np.array_equal(stack24_roundtrip(dev), dev)
+    edge = np.array([0, 1, (1 << 23) - 1, -1, -(1 << 23), 65535, 65536, -65536, -65537])
+    assert np.array_equal(stack24_roundtrip(edge), edge)
+
+
 def test_stack24_fit_rule():
     """6 waves per SIMD need every ref in a 3-byte stack entry: a tree of 2^20 triangles (leaf refs
     below -2^23) and > 2^16 nodes (128-B node offsets >= 2^23) falls back to 5 waves and 4-byte
