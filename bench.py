@@ -88,8 +88,9 @@ def parse():
     p.add_argument("--pipeline", type=int, default=2,
                    help="frames in flight: step k runs on the context's pipeline stream k %% P, so the next "
                         "frame fills the CUs the previous frame's end-of-launch drain leaves idle (1 = serial)")
-    p.add_argument("--check", action="store_true",
-                   help="rank 0 compares the assembled frames with single-launch renders (bit-exact)")
+    p.add_argument("--check", default="auto", choices=["auto", "on", "off"],
+                   help="one untimed step before timing whose gathered frames rank 0 compares bit for bit with "
+                        "single-launch renders of the same seeds (auto: on when N > 1)")
     return p.parse_args()
 
 
@@ -225,6 +226,16 @@ def main():
 
     for k in range(args.warmup):
         step(k, None)
+    # untimed check step (default with N > 1): the frames rank 0 gathered over the
+    # collective equal single-launch renders of the same seeds on rank 0's GPU
+    check = None
+    if args.check == "on" or (args.check == "auto" and world > 1):
+        got = step(0, None)
+        torch.cuda.synchronize()
+        if rank == 0:
+            seeds = np.array([seed for _, seed in frames], np.uint32)
+            refs = ctx.render_frames(w.camera_param(W / H, spp, 0), W, H, seeds)
+            check = all(bool(np.array_equal(got[fid].cpu().numpy(), refs[i])) for i, (fid, _) in enumerate(frames))
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -261,12 +272,6 @@ def main():
                      st["tri_tests"], kern_ms], np.float64)
     simt = {"path_loop": st["loop_lane_iters"] / max(64 * st["loop_wave_iters"], 1),
             "bvh_loop": st["trav_lane_steps"] / max(64 * st["trav_wave_steps"], 1)}
-    check = None
-    if args.check and rank == 0 and img is not None:  # outside the timed region
-        check = True
-        for fid, seed in frames:
-            ref = ctx.render_frames(w.camera_param(W / H, spp, 0), W, H, np.array([seed], np.uint32))[0]
-            check &= bool(np.array_equal(img[fid].cpu().numpy(), ref))
     if world > 1:
         tm = torch.tensor(mine, device=dev if args.dist_backend == "nccl" else "cpu")
         allv = [torch.zeros_like(tm) for _ in range(world)]
@@ -289,12 +294,25 @@ def main():
         bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         survey_bytes = mine[4] * SURVEY_NODE_BYTES + mine[5] * SURVEY_TRI_BYTES + mine[1] * SHADE_BYTES
-        traffic, l2 = None, None
+        # PMC-derived figures (traffic, L2 requests) come from a profile of this exact binary
+        # only: the entry must carry the running library's build id (a hash of the kernel
+        # sources and flags, wgt_build_id), else they are null with the reason
+        build_id = w.build_id()
+        traffic, l2, tj_id = None, None, None
+        traffic_note = "no profile entry for this workload"
         try:
             with open(args.traffic_json) as f:
                 tj = json.load(f)
             tj = tj.get(f"{args.scene}-{W}x{H}-{spp}spp", {})  # one entry per workload
-            if tj.get("n_gpus", 1) == 1 and world == 1 and tj.get("kernel") == kernel:
+            tj_id = tj.get("build_id")
+            if tj and tj_id != build_id:
+                traffic_note = f"profile entry is of build {tj_id}, not the running {build_id}: not applicable"
+            elif tj and (tj.get("n_gpus", 1) != 1 or world != 1):
+                traffic_note = "profiled on 1 GPU; not applicable at N > 1"
+            elif tj and tj.get("kernel") != kernel:
+                traffic_note = f"profile entry is of {tj.get('kernel')}, not the timed {kernel}"
+            if tj and tj_id == build_id and tj.get("n_gpus", 1) == 1 and world == 1 and tj.get("kernel") == kernel:
+                traffic_note = f"PMC passes of build {build_id} ({tj.get('source')})"
                 traffic = tj.get("hbm_bytes_per_launch")
                 req = tj.get("tcc_requests_per_launch")
                 with open(L2_CALIB_JSON) as f:
@@ -346,7 +364,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(survey_bytes / (kern_ms * 1e-3) / 1e9, 2) if kern_ms > 0
                          else 0.0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(survey_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if kern_ms > 0
-                         else 0.0, "traffic": traffic,
+                         else 0.0, "traffic": traffic, "traffic_build_id": tj_id if traffic is not None else None,
+                         "traffic_note": traffic_note,
                          "bytes_per_unit": {"node": SURVEY_NODE_BYTES, "tri": SURVEY_TRI_BYTES,
                                             "shade_per_ray": SHADE_BYTES},
                          # the bytes this implementation's encodings load per launch (80-B compact or 112-B
@@ -362,9 +381,13 @@ def main():
                          "count_spread": {"passes": len(sts), "node_visits": [min(nodes), max(nodes)],
                                           "tri_tests": [min(tris), max(tris)]}},
             "cpu_baseline": base,
+            "build_id": build_id,
         }
         if check is not None:
             line["check_frames_bit_exact"] = check
+            line["check"] = {"frames": len(frames), "world_size": world,
+                             "collective": "rccl" if args.dist_backend == "nccl" else "gloo",
+                             "against": "ctx.render_frames of the same seeds on rank 0 (one launch)"}
         print(json.dumps(line), flush=True)
     # teardown: the process group and torch's buffers may still refer to the context's
     # pipeline streams, so they go first; the context (which destroys its streams) last

@@ -145,6 +145,9 @@ int wgt_create(int hip_device, wgt_ctx **out);
 void wgt_destroy(wgt_ctx *ctx); /* idempotent for NULL */
 const char *wgt_last_error(const wgt_ctx *ctx); /* ctx may be NULL */
 int wgt_version(void);
+/* 16 hex digits identifying the kernel build (a hash of the HIP sources, the headers
+ * they include and the compile flags): profiles key their counters by it (bench.py) */
+const char *wgt_build_id(void);
 int wgt_device_count(int *count);
 
 /* ---- scene upload (replaces Scene::InitBuffers) ------------------------- */

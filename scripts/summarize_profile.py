@@ -43,7 +43,7 @@ def main():
     shutil.copy(os.path.join(src, "kt", "run_kernel_stats.csv"), os.path.join(dst, f"{rnd}_{tag}_kernel_stats.csv"))
     bench = open(os.path.join(src, "bench.log")).read().strip().splitlines()[-1]
     line = json.loads(bench)
-    out = [f"# {rnd} profile `{tag}` — {line['config']['workload']}", "",
+    out = [f"# {rnd} profile `{tag}` — {line['config']['workload']}, build {line.get('build_id')}", "",
            "rocprofv3 --kernel-trace --stats (same bench command, 4 timed steps, 2 frames in flight):", "", "| kernel | calls | avg ms |",
            "|---|---|---|"]
     for r in csv.DictReader(open(os.path.join(src, "kt", "run_kernel_stats.csv"))):
@@ -102,8 +102,10 @@ def main():
         if "workload" in table:  # the old single-entry format
             table = {table["workload"]: table}
         wl = line["config"]["workload"]
-        table[wl] = {"workload": wl, "n_gpus": 1, "kernel": timed, "hbm_bytes_per_launch": hbm,
-                     "fetch_size_kib": fetch, "write_size_kib": write, "source": f"profiles/{rnd}_{tag}_summary.md"}
+        # the build the counters were measured on (bench.py applies them to that build only)
+        table[wl] = {"workload": wl, "n_gpus": 1, "kernel": timed, "build_id": line.get("build_id"),
+                     "hbm_bytes_per_launch": hbm, "fetch_size_kib": fetch, "write_size_kib": write,
+                     "source": f"profiles/{rnd}_{tag}_summary.md"}
         if hit + miss > 0:  # L2 requests of the timed kernel (bench.py's roofline.l2)
             table[wl]["tcc_requests_per_launch"] = hit + miss
             table[wl]["tcc_hit_rate"] = round(hit / (hit + miss), 4)

@@ -53,6 +53,15 @@ def test_version(wgt):
     assert _lib.lib().wgt_version() == 1
 
 
+def test_build_id_names_the_kernel_sources(wgt):
+    """wgt_build_id = the Makefile's hash of the HIP sources, their headers and the flags
+    (bench.py keys the PMC traffic of profiles/pmc_traffic.json by it)."""
+    bid = wgt.build_id()
+    assert re.fullmatch(r"[0-9a-f]{16}", bid)
+    gen = open(os.path.join(ROOT, "webgputracer_amd", "build", "build_id.cpp")).read()
+    assert f'"{bid}"' in gen
+
+
 def test_no_device_fails_loudly(wgt):
     """Without a GPU the product refuses to run (no CPU fallback exists)."""
     if wgt.device_count() > 0:

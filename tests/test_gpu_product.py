@@ -222,3 +222,52 @@ def test_pipelined_launches_vs_oracle(ctx, wgt, oracle):
     osc.close()
     with pytest.raises(Exception):
         ctx.pipeline_stream(4)
+
+
+def test_frames_launcher_two_ranks_union(tmp_path, wgt):
+    """C5's replica launcher with two ranks (settings/run.py:11-24 splits a frame range
+    over machines; here RANK/WORLD_SIZE deal frames round-robin, frames.py
+    frames_of_rank): two fresh processes on cuda:0 write disjoint file sets whose
+    union is 000.png .. 005.png (render.cpp:437-439, 494-497), each file byte-equal to
+    a single-process run's."""
+    common = [sys.executable, "-m", "webgputracer_amd.frames", "--frame", "1", "6", "--width", "64", "--height", "36",
+              "--spp", "4", "--scene", "bunny", "--batch", "2"]
+    single = tmp_path / "single"
+    single.mkdir()
+    r = subprocess.run(common + ["--out", str(single)], capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout + r.stderr
+    procs, dirs = [], []
+    for rank in range(2):
+        d = tmp_path / f"rank{rank}"
+        d.mkdir()
+        dirs.append(d)
+        env = dict(os.environ, RANK=str(rank), WORLD_SIZE="2", LOCAL_RANK=str(rank))
+        procs.append(subprocess.Popen(common + ["--out", str(d)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                                      text=True, cwd=ROOT, env=env))
+    for p in procs:
+        out, _ = p.communicate(timeout=300)
+        assert p.returncode == 0, out
+    sets = [{p.name: p.read_bytes() for p in sorted(d.glob("*.png"))} for d in dirs]
+    assert not set(sets[0]) & set(sets[1]), "ranks rendered a frame twice"
+    assert sorted(sets[0]) == ["000.png", "002.png", "004.png"]  # i = start-1 .. end-1, dealt round-robin
+    union = {**sets[0], **sets[1]}
+    ref = {p.name: p.read_bytes() for p in sorted(single.glob("*.png"))}
+    assert sorted(union) == [f"{i:03d}.png" for i in range(6)] == sorted(ref)
+    assert union == ref
+
+
+def test_bench_two_ranks_self_checks(tmp_path):
+    """bench.py at N = 2 (torch.distributed.run, gloo, both ranks on cuda:0) runs its
+    untimed check step without being asked: the line carries check_frames_bit_exact =
+    true, i.e. the frames gathered over the collective equal single-launch renders."""
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--dist-backend", "gloo", "--scene", "bunny", "--width", "96", "--height", "64", "--spp", "4",
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--stats-reps", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["check_frames_bit_exact"] is True
+    assert line["check"]["world_size"] == 2 and line["check"]["frames"] == 2

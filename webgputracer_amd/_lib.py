@@ -60,7 +60,7 @@ class WgtSceneInfo(ctypes.Structure):
 
 # Every symbol include/wgt_api.h declares (checked by tests/test_abi.py).
 EXPORTS = [
-    "wgt_create", "wgt_destroy", "wgt_last_error", "wgt_version", "wgt_device_count",
+    "wgt_create", "wgt_destroy", "wgt_last_error", "wgt_version", "wgt_build_id", "wgt_device_count",
     "wgt_upload_scene", "wgt_scene_info_get", "wgt_render_tile", "wgt_render_tiles_async",
     "wgt_render_tiles_stats", "wgt_render_tiles_profile", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_selftest_math", "wgt_stream",
     "wgt_pipeline_stream",
@@ -100,6 +100,7 @@ def lib():
         "wgt_destroy": (None, [P]),
         "wgt_last_error": (ctypes.c_char_p, [P]),
         "wgt_version": (I, []),
+        "wgt_build_id": (ctypes.c_char_p, []),
         "wgt_device_count": (I, [ctypes.POINTER(I)]),
         "wgt_upload_scene": (I, [P, P, U32, P, U32, P, U32, P, U32]),
         "wgt_scene_info_get": (I, [P, ctypes.POINTER(WgtSceneInfo)]),

@@ -209,8 +209,9 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             if (STATS) { ++c.q; ++c.nan; }
             nanray = false;
           } else {
-            WGT_REGION(cr_fin, float4 pre[2]; preload_tshade(sc, t, pre[0], pre[1]);
-                       quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h, pre));
+            // no triangles (TRIS = false): no shading record exists to preload
+            WGT_REGION(cr_fin, float4 pre[2]; if (TRIS) preload_tshade(sc, t, pre[0], pre[1]);
+                       quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h, TRIS ? pre : nullptr));
             if (STATS) { ++c.q; ++c.tr; }
           }
           first_hit(px, depth, h.prim, po, outhit);
@@ -368,7 +369,7 @@ k_lpt_order(const uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __rest
 //             denormals);
 //   div_rn    on n pseudo-random (numerator, denominator) pairs from the quad plane
 //             distance's range under the render limits: |n| <= 2^44 of any exponent
-//             (zeros and denormals included), 2^-10 <= |d| <= 2^33 (|d| >= kRayMin is
+//             (zeros and denormals included), 2^-10 <= |d| < 2^35 (|d| >= kRayMin is
 //             tested before the division): the accept decision t in [kRayMin,
 //             kRayMax] must equal the IEEE one, and an accepted t its bits;
 //   the compiler's own lowerings (__builtin_sqrtf, n / d) on the same inputs.
@@ -407,7 +408,7 @@ __global__ void __launch_bounds__(256) k_selftest_math(uint32_t n, uint32_t seed
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint32_t)stride) {
     const uint32_t h = st_hash(seed * 0x9e3779b9u + i), h2 = st_hash(h ^ 0x5bd1e995u);
     const float nn = st_float(h, 0u, 127u + 44u);             // |n| <= 2^45 (zeros, denormals)
-    const float dd = st_float(h2, 127u - 10u, 127u + 32u);    // 2^-10 <= |d| < 2^33
+    const float dd = st_float(h2, 127u - 10u, 127u + 34u);    // 2^-10 <= |d| < 2^35 (bound 2*sqrt(3)*2^32)
     const float ref = (float)((double)nn / (double)dd);
     const float q = div_rn(nn, dd);
     const bool acc = st_accept(ref);

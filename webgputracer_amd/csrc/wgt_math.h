@@ -91,7 +91,8 @@ WGT_HD float sqrt_rn(float x) {
 // plane distance t = n / denom (isect_quad), is exact wherever the result decides
 // anything: |denom| >= kRayMin is tested first, and the scene and frame limits
 // checked at upload and per render (wgt_runtime.cpp) bound
-// |denom| <= 2^33 and |n| <= 2^44, so a quotient in the accepted [kRayMin, kRayMax]
+// |denom| <= |qn| |d| <= 2*sqrt(3) * 2^32 < 2^35 (normal components within 2, primary
+// directions within 2^32) and |n| <= 2^44, so a quotient in the accepted [kRayMin, kRayMax]
 // is in the domain, and one outside it comes out outside it too (|q| < 2^-80 or
 // > 2^100 cannot turn into [kRayMin, kRayMax]).
 WGT_HD float div_rn(float n, float d) {

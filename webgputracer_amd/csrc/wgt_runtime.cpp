@@ -150,6 +150,9 @@ double narrow_ratio() { return env_u32("WGT_NARROW", 0) == 2 ? 1e30 : kNarrowNod
 // k_render_ps waves per SIMD (DevScene::ps_waves): 6 with 3-byte stack entries when
 // every ref fits them, else 5; WGT_PS_WAVES=5 forces 5 (sweeps).
 uint32_t ps_waves_for(const BvhOut& bvh, uint32_t n_tris) {
+  // no triangles: the kernel without traversal (4-byte stack bytes in the launch and
+  // the occupancy query alike, ps_stack_lds_bytes)
+  if (n_tris == 0) return (uint32_t)kPsWavesNoTris;
   if (env_u32("WGT_PS_WAVES", 0) == 5) return 5u;
   return bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris ? 6u : 5u;
 }
@@ -467,8 +470,11 @@ int wgt_create(int hip_device, wgt_ctx** out) {
 void wgt_destroy(wgt_ctx* ctx) {
   if (!ctx) return;
   (void)hipSetDevice(ctx->device);
-  if (ctx->use_ev) (void)hipEventSynchronize(ctx->use_ev);  // launches on callers' streams too
-  if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+  // every launch that may read the scene or a buffer of the context (trace queries,
+  // the workspace slots' renders on any stream, the context stream) ends first
+  (void)use_drain(ctx);
+  for (hipStream_t p : ctx->pipe)
+    if (p) (void)hipStreamSynchronize(p);
   if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
   free_buf(ctx->tiles); free_buf(ctx->out8); free_buf(ctx->out32); free_buf(ctx->hit);
   free_buf(ctx->counters); free_buf(ctx->rays); free_buf(ctx->prim); free_buf(ctx->dist);

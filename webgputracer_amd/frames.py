@@ -129,10 +129,17 @@ def main(argv=None):
     a = ap.parse_args(argv)
     if a.frame[0] < 1 or a.frame[1] < a.frame[0]:
         ap.error("bad frame range")  # the C++ CLI's check (csrc/main.cpp)
+    if not 1 <= a.pipeline <= 4:
+        ap.error("--pipeline must be 1..4 (the context has 4 pipeline streams)")
+    if a.batch < 1:
+        ap.error("--batch must be >= 1")
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+
+    # one process per GPU; ranks beyond the visible GPUs share them (rehearsals, tests)
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(torch.cuda.device_count(), 1)
     if a.scene == "cornell":
         scene = cornell_scene()
     elif a.scene.startswith("obj:"):
@@ -151,8 +158,6 @@ def main(argv=None):
             for f in b:
                 write_png(os.path.join(a.out, f"{f:03d}.png"), imgs[f])  # render.cpp:494-497
     dt = time.perf_counter() - t0
-    import torch
-
     torch.cuda.synchronize()
     print(json.dumps({"rank": rank, "world": world, "frames": len(mine), "batch": a.batch, "pipeline": a.pipeline,
                       "seconds": round(dt, 3),

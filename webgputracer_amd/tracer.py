@@ -122,6 +122,11 @@ def camera_param(aspect: float, spp: int, seed: int, fovy: float = 40.0):
     return cam
 
 
+def build_id() -> str:
+    """The loaded library's kernel build id (wgt_build_id: hash of the HIP sources and flags)."""
+    return lib().wgt_build_id().decode()
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     rc = lib().wgt_device_count(ctypes.byref(n))
