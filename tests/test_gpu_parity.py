@@ -312,14 +312,18 @@ _SCHED_REF = {}
                                  {"WGT_PS_SVC_FRAC": "1"},
                                  {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
                                  {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}, {"WGT_NARROW": "1"},
-                                 {"WGT_STACK_LIMIT": "20"}])
+                                 {"WGT_STACK_LIMIT": "20"},
+                                 # the workgroup ray pool (wgt_pool.hip, opt-in): rays move between lanes
+                                 {"WGT_POOL": "6"}, {"WGT_POOL": "5"}, {"WGT_POOL": "6", "WGT_CNODE": "1"},
+                                 {"WGT_POOL": "5", "WGT_PS_TO_TRAV": "48", "WGT_PS_TO_SERVICE": "46"}])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the
     cost pre-pass (1 or 4 spp) or block order; refill threshold; phase thresholds and
     their sparse-wave scaling; the node form: compact nodes forced on the bunny; the
     wave budget: 6 waves per SIMD with 3-byte stack entries or, with WGT_PS_WAVES=5, 5
     with 4-byte ones; the narrow 25-entry tree, WGT_NARROW=1; a 20-entry bound, which moves
-    the 3-byte stack's byte array)
+    the 3-byte stack's byte array; the workgroup ray pool, WGT_POOL, whose rays are
+    traversed by lanes of other waves)
     change which lane renders which pixel and when, never a bit of the result.  100x60
     leaves ragged 8x8 blocks at the frame edge.  The test runs after the kernel-family
     tests on the same context, the sequence that exposed a workspace-reuse bug (each

@@ -359,20 +359,26 @@ constexpr int kNoRef = 0x7fffffff;
 // of a tree with fewer than 2^16 nodes and 2^20 triangles (byte offsets < 2^23,
 // leaf refs >= -2^23; DevScene::ps_waves) and lets LDS hold the full 31-entry
 // bound of 24 waves per CU: 6 waves per SIMD without a narrower tree.
-struct Stack32 {
+// S: the stride in entries (kBlock for one wave per block; the ray-pool kernel's
+// workgroup-wide columns use its block size, wgt_pool.hip).
+template <int S = kBlock>
+struct Stack32S {
   int* __restrict__ p;
-  __device__ __forceinline__ int ld(int i) const { return p[i * kBlock]; }
-  __device__ __forceinline__ void st(int i, int v) const { p[i * kBlock] = v; }
+  __device__ __forceinline__ int ld(int i) const { return p[i * S]; }
+  __device__ __forceinline__ void st(int i, int v) const { p[i * S] = v; }
 };
-struct Stack24 {
+template <int S = kBlock>
+struct Stack24S {
   uint16_t* __restrict__ lo;
   int8_t* __restrict__ hi;
-  __device__ __forceinline__ int ld(int i) const { return ((int)hi[i * kBlock] << 16) | (int)lo[i * kBlock]; }
+  __device__ __forceinline__ int ld(int i) const { return ((int)hi[i * S] << 16) | (int)lo[i * S]; }
   __device__ __forceinline__ void st(int i, int v) const {
-    lo[i * kBlock] = (uint16_t)v;
-    hi[i * kBlock] = (int8_t)(v >> 16);
+    lo[i * S] = (uint16_t)v;
+    hi[i * S] = (int8_t)(v >> 16);
   }
 };
+using Stack32 = Stack32S<>;
+using Stack24 = Stack24S<>;
 
 // Place `cand` (a child ref, or kNoRef = take the next stack entry).
 template <class STK>
@@ -459,23 +465,28 @@ __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t
 // PRELOAD: the triangle's shading record is read before the quad hit is rebuilt (the
 // caller issues both loads together, preload_tshade) instead of after the distance
 // comparison that needs it: one memory round trip per finalise instead of two.
-__device__ __forceinline__ void preload_tshade(const DevScene& sc, const Trav& t, float4& s0, float4& s1) {
-  const uint32_t i = trav_found(t) ? t.bi : 0u;  // record 0 for a ray without a triangle hit: unused
+// The triangle result of a finished traversal: (bt, bi), bi = kNoHit when no
+// triangle was accepted (trav_found).
+__device__ __forceinline__ void preload_tshade(const DevScene& sc, uint32_t bi, float4& s0, float4& s1) {
+  const uint32_t i = bi != kNoHit ? bi : 0u;  // record 0 for a ray without a triangle hit: unused
   s0 = sc.tshade[2 * i];
   s1 = sc.tshade[2 * i + 1];
 }
-__device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const Trav& t, Hit& h,
+__device__ __forceinline__ void preload_tshade(const DevScene& sc, const Trav& t, float4& s0, float4& s1) {
+  preload_tshade(sc, t.bi, s0, s1);
+}
+__device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, float bt, uint32_t bi, Hit& h,
                                            const float4* pre = nullptr) {
   const uint32_t nlq = sc.n_lights + sc.n_quads;
-  if (trav_found(t)) {
-    const f3 pos = o + t.bt * d;
+  if (bi != kNoHit) {
+    const f3 pos = o + bt * d;
     const float ray_dist = distance(pos, o);
     if (!(ray_dist >= h.dist)) {
-      const float4 s0 = pre ? pre[0] : sc.tshade[2 * t.bi], s1 = pre ? pre[1] : sc.tshade[2 * t.bi + 1];
+      const float4 s0 = pre ? pre[0] : sc.tshade[2 * bi], s1 = pre ? pre[1] : sc.tshade[2 * bi + 1];
       const f3 fn = xyz(s0);
       const bool ff = dot(d, fn) < 0.0f;
       h.dist = ray_dist;
-      h.prim = nlq + t.bi;
+      h.prim = nlq + bi;
       h.emissive = s0.w > 0.0f;
       h.front_face = ff;
       h.pos = pos;
@@ -485,6 +496,10 @@ __device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const
   }
   for (uint32_t k = 0; k < sc.n_spheres; ++k)
     isect_sphere(o, d, sc.spheres + 2 * k, nlq + sc.n_tris + k, h);
+}
+__device__ __forceinline__ void finish_hit(const DevScene& sc, f3 o, f3 d, const Trav& t, Hit& h,
+                                           const float4* pre = nullptr) {
+  finish_hit(sc, o, d, t.bt, t.bi, h, pre);
 }
 
 // Full sample_hit for one ray (k_trace with EXACT, k_render).

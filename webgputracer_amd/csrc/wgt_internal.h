@@ -109,7 +109,11 @@ struct DevFrame {
   uint32_t pq_svc_cost;  // pre-pass work units per ray started (a service iteration ~ 7 traversal steps)
   const uint32_t* perm;
   uint32_t* cost;
-
+  // ray pool (k_render_pool, wgt_pool.hip): 0 = off (k_render_ps), else the pool kernel's
+  // waves per SIMD (6 or 5); ray tickets per wave; idle lanes that trigger an adoption;
+  // whether a wave leaving its traversal parks its own unfinished rays; resident
+  // workgroups on the device (set by the runtime)
+  uint32_t pool, pool_tickets, pool_adopt_min, pool_park, pool_resident;
 };
 
 // Wavefront path state, SoA over slots (one slot per pixel of the tile list).
@@ -176,6 +180,12 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
 bool use_compact_nodes(const DevScene& sc, const DevFrame& fr);
 // Waves of k_render_ps resident on the whole device for this scene's LDS stack.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves);
+// The ray-pool kernel (wgt_pool.hip): launched by launch_render when fr.pool is set.
+hipError_t launch_pool(const DevScene& sc, const DevFrame& f, bool cn, uint32_t resident_wgs, const wgt_tile* tiles,
+                       uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters, uint32_t* queue,
+                       hipStream_t stream);
+uint32_t pool_tickets_for(int w);  // ray tickets per wave of the pool kernel at w waves per SIMD
+hipError_t pool_resident_wgs(int w, int device, uint32_t& wgs);
 hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d_counts, hipStream_t stream);
 hipError_t launch_trace(const DevScene& sc, const float* d_rays, uint32_t n, uint32_t* prim,
                         float* dist, hipStream_t stream);

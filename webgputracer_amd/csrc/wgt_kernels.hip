@@ -504,7 +504,10 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       f.perm = fc.cost + nb;
       e = hipGetLastError();
     }
-    if (e == hipSuccess) {
+    if (e == hipSuccess && f.pool && tris && sc.ps_waves == 6 && f.pool_tickets && f.pool_resident) {
+      // the ray-pool kernel (wgt_pool.hip); the cost pre-pass above stays k_render_ps
+      e = launch_pool(sc, f, cn, f.pool_resident, d_tiles, out8, out32, outhit, counters, q + 1, stream);
+    } else if (e == hipSuccess) {
       if (counters) ps_launch<true, false>(sc, cn, grid, block, plds, stream, f, d_tiles, out8, out32, outhit, counters, q + 1);
       else ps_launch<false, false>(sc, cn, grid, block, plds, stream, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
       e = hipGetLastError();

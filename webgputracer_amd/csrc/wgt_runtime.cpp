@@ -50,6 +50,9 @@ struct wgt_ctx {
   DevBuf wf, ctl;
   unsigned long long* ctl_host = nullptr;
   uint32_t ps_resident = 0;
+  // the ray-pool kernel per waves-per-SIMD budget (index 0: 6, 1: 5): tickets per wave
+  // that keep 6 (5) workgroups per CU, and the resident workgroups at that LDS size
+  uint32_t pool_tickets[2] = {0, 0}, pool_resident[2] = {0, 0};
   // Scheduling workspaces of the persistent kernel (queues, LPT costs and order),
   // used round-robin by its launches.  A launch waits (on the device) only for the
   // previous launch that used the same slot, so consecutive frames issued on two
@@ -202,6 +205,11 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   fr.pq_svc_cost = env_u32("WGT_PQ_SVC_COST", 7);
   fr.pq_lpt_all = env_u32("WGT_PQ_LPT_ALL", 1);  // sweep: all pixels -3% (sponza), -4% (bunny) at 256 spp
+  // the workgroup ray pool (wgt_pool.hip): WGT_POOL = 6 or 5 (waves per SIMD), 0 = off
+  fr.pool = env_u32("WGT_POOL", 0);
+  if (fr.pool != 5 && fr.pool != 6) fr.pool = 0;
+  fr.pool_adopt_min = std::max(env_u32("WGT_POOL_ADOPT", 1), 1u);
+  fr.pool_park = env_u32("WGT_POOL_PARK", 1);
   return fr;
 }
 
@@ -357,7 +365,13 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
     if ((rc = ensure(ctx, sl.ws, ws_need))) return rc;
     if (!sl.ev) WGT_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
     else WGT_HIP(ctx, hipStreamWaitEvent(s, sl.ev, 0));
-    WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
+    DevFrame f = fr;
+    if (f.pool) {
+      const int i = f.pool == 6 ? 0 : 1;
+      f.pool_tickets = ctx->pool_tickets[i];
+      f.pool_resident = ctx->pool_resident[i];
+    }
+    WGT_HIP(ctx, launch_render(ctx->sc, f, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
                                sl.ws.p, sl.ws.bytes, s));
     WGT_HIP(ctx, hipEventRecord(sl.ev, s));
     if (timing) {
@@ -678,6 +692,17 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
   sc.ps_waves = ps_waves_for(bvh, n_tris);
   WGT_HIP(ctx, ps_resident_waves(sc, ctx->device, ctx->ps_resident));
+  for (int i = 0; i < 2; ++i) {
+    ctx->pool_tickets[i] = ctx->pool_resident[i] = 0;
+    if (n_tris == 0 || sc.ps_waves != 6) continue;  // the pool records pack 24-bit refs
+    const int w = i == 0 ? 6 : 5;
+    ctx->pool_tickets[i] = pool_tickets_for(w);
+    WGT_HIP(ctx, pool_resident_wgs(w, ctx->device, ctx->pool_resident[i]));
+  }
+  if (env_u32("WGT_DEBUG", 0))
+    std::fprintf(stderr, "[wgt] resident: k_render_ps %u waves; pool(6) %u workgroups, %u tickets; "
+                         "pool(5) %u workgroups, %u tickets\n", ctx->ps_resident, ctx->pool_resident[0],
+                 ctx->pool_tickets[0], ctx->pool_resident[1], ctx->pool_tickets[1]);
 
   wgt_scene_info& in = ctx->info;
   in = wgt_scene_info{};
