@@ -232,8 +232,9 @@ int wgt_sync(wgt_ctx *ctx);
  * sqrt_fast, div_rn) against correctly rounded results (the f64 operation rounded
  * to f32): sqrt_rn on all 2^32 inputs, sqrt_fast on every input of its domain,
  * div_rn on n pseudo-random operand pairs of the quad distance under the render
- * limits (accept decision and accepted bits).  counts[0..7] = sqrt tests (2^32),
- * sqrt_rn mismatches, div tests (n), div_rn mismatches, sqrt_fast tests,
+ * limits (accept decision and accepted bits) and on n Moller-Trumbore reciprocals
+ * 1/det (bits).  counts[0..7] = sqrt tests (2^32),
+ * sqrt_rn mismatches, div tests (2n), div_rn mismatches, sqrt_fast tests,
  * sqrt_fast mismatches, and the mismatches of the compiler's own f32 sqrt and
  * division on the same inputs (synchronous). */
 int wgt_selftest_math(wgt_ctx *ctx, uint32_t n, uint32_t seed, uint64_t counts[8]);

@@ -35,7 +35,12 @@ out = {"scene": scene, "spp": spp, "pool": pool, "ms": round(pr["kernel_ms"], 3)
        "trav_wave_steps": st["trav_wave_steps"], "svc_wave_iters": st["loop_wave_iters"],
        "nodes": st["node_visits"], "tris": st["tri_tests"], "traced": st["traced_rays"],
        "cyc_service": st["cyc_service"], "cyc_trav": st["cyc_trav"]}
-if pool != "0":
+if pool == "0":  # k_render_ps: wave cycles per service-phase region (STATS, WGT_REGION)
+    out["svc_regions"] = {k[4:]: round(st[k] / max(st["cyc_service"], 1), 4) for k in
+                          ("cyc_refill", "cyc_finalise", "cyc_shade", "cyc_camera", "cyc_quads", "cyc_root")}
+    out["svc_cyc_per_pass"] = round(st["cyc_service"] / max(st["loop_wave_iters"], 1), 1)
+    out["trav_cyc_per_step"] = round(st["cyc_trav"] / max(st["trav_wave_steps"], 1), 1)
+else:
     out.update({"adopt": st["cyc_refill"], "miss": st["cyc_finalise"], "park": st["cyc_shade"],
                 "return": st["cyc_camera"], "stash": st["cyc_quads"], "phases": st["cyc_root"]})
 print(json.dumps(out), flush=True)

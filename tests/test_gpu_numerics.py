@@ -90,8 +90,9 @@ def test_scaled_mesh_vs_oracle(ctx, wgt, oracle, log2s, cnode, monkeypatch):
 
 def test_render_limits_fail_cleanly(ctx, wgt):
     """Outside the numeric limits that keep the quad distance's short division exact
-    (scene coordinates and camera within 2^40, quad normals within 2 or NaN, primary
-    directions within 2^32; wgt_runtime.cpp check_scene_limits / check_render_args)
+    (scene coordinates and camera within 2^40, quad normals within 2 or NaN, triangle
+    edges within 2^30, primary directions within 2^32; wgt_runtime.cpp
+    check_scene_limits / check_render_args)
     the calls return WGT_E_INVALID instead of rendering."""
     from webgputracer_amd._lib import WGT_E_INVALID, WgtError
 
@@ -112,6 +113,9 @@ def test_render_limits_fail_cleanly(ctx, wgt):
     T = wgt.procedural_mesh("bunny", 500)
     T["v0"][7, 1] = np.inf
     invalid(lambda: ctx.upload_scene(L, Q[:5], S, T))
+    T = wgt.procedural_mesh("bunny", 500)
+    T["e2"][3, 2] = 2.0 ** 31  # an edge beyond 2^30 (Moller-Trumbore's short 1/det)
+    invalid(lambda: ctx.upload_scene(L, Q[:5], S, T))
     Qd = Q.copy()
     Qd["norm"][4, :3] = np.nan  # a degenerate quad's NaN normal is accepted
     ctx.upload_scene(L, Qd, S)
@@ -127,10 +131,13 @@ def test_selftest_math_sequences_are_exact(ctx, seed):
     """sqrt_rn equals correctly rounded sqrt on all 2^32 inputs, sqrt_fast on every
     input of its domain; div_rn gives the IEEE accept decision and accepted bits on
     16M quad-distance operand pairs under the render limits (zeros, denormals and
-    every exponent of the numerator included)."""
+    every exponent of the numerator included; denominators up to 2^35, the bound
+    2*sqrt(3)*2^32 of |qn . d|), and the IEEE bits of 1/det on 16M determinants over
+    Moller-Trumbore's range 2^-40 <= |det| < 2^95 under the limits."""
     c = ctx.selftest_math(1 << 24, seed)
     print("selftest", c)
-    assert c["sqrt_tests"] == 1 << 32 and c["div_tests"] == 1 << 24 and c["sqrt_fast_tests"] > 3 << 30
+    # div_tests: 2^24 quad-distance quotients + 2^24 Moller-Trumbore reciprocals 1/det
+    assert c["sqrt_tests"] == 1 << 32 and c["div_tests"] == 2 << 24 and c["sqrt_fast_tests"] > 3 << 30
     assert c["sqrt_rn_bad"] == 0 and c["sqrt_fast_bad"] == 0 and c["div_rn_bad"] == 0, c
 
 

@@ -147,6 +147,39 @@ __device__ __forceinline__ void simt_count(uint32_t& wave, uint32_t& lane) {
   ++lane;
 }
 
+// One triangle test of the record at byte offset lf (wgt_geom.h kTriRecordBytes):
+// Moller-Trumbore, then for a candidate that beats (bt, bi) the slab check against the
+// triangle's own padded box.  inv: 1/d.  Returns true with (tt, idx)
+// when the triangle becomes the closest hit.
+// SHORT: mt_test's short reciprocal (render rays only, wgt_geom.h).
+template <bool SHORT>
+__device__ __forceinline__ bool tri_test(const DevScene& sc, uint32_t lf, f3 o, f3 d, f3 ot, f3 inv, float bt,
+                                         uint32_t bi, float& tt, uint32_t& idx) {
+  const char* __restrict__ p = (const char*)sc.tris + lf;
+  f3 v0, e1, e2, blo, bhi;
+  if (kTriRecordBytes == 64) {
+    // all four float4 of the record at once: the padded box D (for a candidate closest
+    // hit) used to be loaded in the branch, a second dependent round trip
+    const float4 A = ((const float4*)p)[0], B = ((const float4*)p)[1], C = ((const float4*)p)[2],
+                 D = ((const float4*)p)[3];
+    v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
+    idx = __float_as_uint(A.w);
+    blo = f3{B.w, C.w, D.x};
+    bhi = f3{D.y, D.z, D.w};
+  } else {
+    const float4 A = *(const float4*)p, B = *(const float4*)(p + 16);
+    const float2 C = *(const float2*)(p + 32);
+    v0 = xyz(A), e1 = xyz(B), e2 = f3{B.w, C.x, C.y};
+    idx = __float_as_uint(A.w);
+  }
+  if (!mt_test<SHORT>(o, d, v0, e1, e2, tt)) return false;
+  if (!(tt < bt || (tt == bt && idx < bi))) return false;
+  if (kTriRecordBytes != 64) tri_box(v0, e1, e2, blo, bhi);
+  float bn, bf;
+  slab(ot, inv, blo, bhi, bn, bf);
+  return bn <= tt && tt <= bf;
+}
+
 // Resumable BVH4 traversal: closest triangle = min (t, index) with t < bound (or
 // t <= bound and index < bi when bi = kNoHit).  Per-lane stack: DevScene::stack
 // entries in LDS (stride kBlock, conflict-free).
@@ -285,21 +318,12 @@ __device__ __forceinline__ bool trav_step(const DevScene& sc, f3 o, f3 d, Trav& 
   bool pop;
   int next = 0;
   if (t.lf < t.le) {
-    const float4* __restrict__ tp = (const float4*)((const char*)sc.tris + t.lf);
-    const float4 A = tp[0], B = tp[1], C = tp[2];
     if (STATS) st.tris++;
     float tt;
-    if (mt_test(o, d, xyz(A), xyz(B), xyz(C), tt)) {
-      const uint32_t idx = __float_as_uint(A.w);
-      if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
-        const float4 D = tp[3];
-        float bn, bf;
-        slab(t.ot, t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
-        if (bn <= tt && tt <= bf) {
-          t.bt = tt;
-          t.bi = idx;
-        }
-      }
+    uint32_t idx;
+    if (tri_test<false>(sc, t.lf, o, d, t.ot, t.inv, t.bt, t.bi, tt, idx)) {  // IEEE: k_trace's rays
+      t.bt = tt;
+      t.bi = idx;
     }
     t.lf += kTriRecordBytes;
     if (t.lf < t.le) return false;
@@ -415,12 +439,14 @@ __device__ __forceinline__ bool trav_done(const Trav& t) { return t.ref == kNoRe
 // visits.  Any order is exact (the closest hit is a minimum
 // over (t, index)), and a missed child's kMissKey keeps it off the stack wherever it
 // sits: each push advances the top only for a hit.
-template <bool STATS, bool CN, class STK>
+// ROOT: the step of a ray that has just started (t.ref = 0 for every lane): the node's
+// address is uniform, so its loads are scalar (SMEM) loads shared by the wave.
+template <bool STATS, bool CN, class STK, bool ROOT = false>
 __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
   if (STATS) st.nodes++;
   uint32_t k0, k1, k2, k3;
   int r0, r1, r2, r3;
-  node_keys<CN>(sc, t, t.ref, k0, k1, k2, k3, r0, r1, r2, r3);
+  node_keys<CN>(sc, t, ROOT ? 0 : t.ref, k0, k1, k2, k3, r0, r1, r2, r3);
   cas(k0, r0, k1, r1);
   cas(k2, r2, k3, r3);
   cas(k0, r0, k2, r2);
@@ -433,28 +459,23 @@ __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, const STK
   trav_resolve(sc, t, k0 != kMissKey ? r0 : kNoRef, lds);
 }
 
+template <bool STATS, bool CN, class STK>
+__device__ __forceinline__ void root_step(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
+  node_step<STATS, CN, STK, true>(sc, t, lds, st);
+}
+
 // Test the next triangle of the pending leaf; a lane without a node to visit
 // takes the next stack entry once its leaf is done.
 template <bool STATS, bool CN = false, class STK>
 __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, const STK& lds,
                                          TravStats& st) {
-  const float4* __restrict__ tp = (const float4*)((const char*)sc.tris + t.lf);
-  // all four float4 of the record at once: the padded box D (for a candidate
-  // closest hit) used to be loaded in the branch, a second dependent round trip
-  const float4 A = tp[0], B = tp[1], C = tp[2], D = tp[3];
   if (STATS) st.tris++;
   float tt;
-  if (mt_test(o, d, xyz(A), xyz(B), xyz(C), tt)) {
-    const uint32_t idx = __float_as_uint(A.w);
-    if (tt < t.bt || (tt == t.bt && idx < t.bi)) {
-      float bn, bf;
-      // 1/d: under CN t.inv holds s/d, and (s/d) * (1/s) is 1/d exactly
-      slab(t.ot, CN ? sc.rcstep * t.inv : t.inv, f3{B.w, C.w, D.x}, f3{D.y, D.z, D.w}, bn, bf);
-      if (bn <= tt && tt <= bf) {
-        t.bt = tt;
-        t.bi = idx;
-      }
-    }
+  uint32_t idx;
+  // 1/d: under CN t.inv holds s/d, and (s/d) * (1/s) is 1/d exactly
+  if (tri_test<true>(sc, t.lf, o, d, t.ot, CN ? sc.rcstep * t.inv : t.inv, t.bt, t.bi, tt, idx)) {
+    t.bt = tt;
+    t.bi = idx;
   }
   t.lf += kTriRecordBytes;
   if (t.lf >= t.le && t.ref == kNoRef) trav_resolve(sc, t, kNoRef, lds);
@@ -540,14 +561,17 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
   // sample_direction (path_tracer.wgsl:146-154)
   const f3 w = normalize(h.norm);  // onb.w of build_onb_from_w(hit.norm)
   f3 sdir;
-  if (rand_next(seed) > 0.5f) {
+  // both branches draw two more rand() (r1 then r2) right away: drawn once here, the
+  // same values in the same order
+  const bool cosine = rand_next(seed) > 0.5f;
+  const float r1 = rand_next(seed);
+  const float r2 = rand_next(seed);
+  if (cosine) {
     // sample_from_cosine: build_onb_from_w (:133-140) + rand_cos_dir (:123-131)
     const f3 a = (sign_w(w.x) * w.x) > 0.9f ? f3{0.0f, 1.0f, 0.0f} : f3{1.0f, 0.0f, 0.0f};
     // |w| = 1 +- 2^-22 and a is the axis w is furthest from: |w x a|^2 >= 0.19
     const f3 v = normalize_unit(cross(w, a));
     const f3 u = cross(w, v);
-    const float r1 = rand_next(seed);
-    const float r2 = rand_next(seed);
     const float z = sqrt_fast(1.0f - r2);
     const float phi = 2.0f * kPI * r1;
     float sphi, cphi;
@@ -558,8 +582,6 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
     sdir = (lx2 * u + ly2 * v) + z * w;
   } else {
     // sample_from_light (:163-168), not normalised
-    const float r1 = rand_next(seed);
-    const float r2 = rand_next(seed);
     sdir = ((L.pos + r1 * L.right) + r2 * L.up) - h.pos;
   }
   // mixture_pdf (:191-193) = 0.5*cosine_pdf + 0.5*light_area_pdf

@@ -67,11 +67,17 @@ WGT_HD f3 slab_offset(f3 o, f3 inv) { return f3{-(o.x * inv.x), -(o.y * inv.y), 
 // them the compiler issues the v0 load with the other two instead of after the
 // determinant (one memory round trip per test instead of two).  Same result: a
 // rejected determinant rejects either way (NaN: not rejected, as before).
+// SHORT: 1/det by the short division div_rn (wgt_math.h), exact for 2^-100 <= |det| <=
+// 2^100.  A |det| < 1e-12 is rejected whatever inv_det is, and for render rays |det| <=
+// |e1| |e2| |d| < 2^94 (triangle edge components within 2^30, wgt_runtime.cpp
+// check_scene_limits; primary directions within 2^32, scattered ones unit), so the
+// result is the IEEE one; caller-supplied rays (k_trace) use IEEE.
+template <bool SHORT = false>
 WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {
   f3 pvec = cross(d, e2);
   float det = dot(e1, pvec);
   const bool det_ok = !(fabs_w(det) < 1e-12f);
-  float inv_det = 1.0f / det;
+  float inv_det = SHORT ? div_rn(1.0f, det) : 1.0f / det;
   f3 tvec = o - v0;
   float u = dot(tvec, pvec) * inv_det;
   if (!det_ok || u < 0.0f || u > 1.0f) return false;
@@ -90,8 +96,16 @@ WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {
 // A-C feed Moller-Trumbore; D (same 128-B line) is read only for a candidate
 // closest hit, to check t against the triangle's own padded box (tri_box,
 // computed by the host builder with the same fp32 operations).
-constexpr int kTriRecordFloats = 16;
-constexpr uint32_t kTriRecordBytes = kTriRecordFloats * 4;  // the kernels walk a leaf by byte offsets
+constexpr int kTriRecordFloats = 16;  // the host / exported record (wgt_bvh_build)
+// The device record the kernels walk (by byte offsets): the 64-B record above, or with
+// WGT_TRI_REC=40 a 40-B one, (v0, index), (e1, e2.x), (e2.y, e2.z), whose padded box is
+// recomputed (tri_box, the builder's own fp32 operations: the same bits) for a
+// candidate closest hit only.
+#ifndef WGT_TRI_REC
+#define WGT_TRI_REC 64
+#endif
+static_assert(WGT_TRI_REC == 64 || WGT_TRI_REC == 40, "triangle record: 64 or 40 bytes");
+constexpr uint32_t kTriRecordBytes = WGT_TRI_REC;
 
 // BVH4 node, 128 B (8 x float4, one L2 cache line), children in SoA order:
 //   N[0] = lo.x of children 0..3   N[1] = hi.x   N[2] = lo.y   N[3] = hi.y

@@ -256,7 +256,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
           if (TRIS) {
-            WGT_REGION(cr_root, node_step<STATS, CN>(sc, t, lds, st));
+            WGT_REGION(cr_root, root_step<STATS, CN>(sc, t, lds, st));
             if (trav_done(t)) pending = true;
             else trav = true;
           } else {
@@ -371,7 +371,9 @@ k_lpt_order(const uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __rest
 //             distance's range under the render limits: |n| <= 2^44 of any exponent
 //             (zeros and denormals included), 2^-10 <= |d| < 2^35 (|d| >= kRayMin is
 //             tested before the division): the accept decision t in [kRayMin,
-//             kRayMax] must equal the IEEE one, and an accepted t its bits;
+//             kRayMax] must equal the IEEE one, and an accepted t its bits; and
+//             the reciprocal 1 / det of Moller-Trumbore (mt_test<true>) for 2^-40 <=
+//             |det| < 2^95 (the render limits' range past the 1e-12 rejection): its bits;
 //   the compiler's own lowerings (__builtin_sqrtf, n / d) on the same inputs.
 // NaN equals NaN.  counts: [0] sqrt tests, [1] sqrt_rn bad, [2] div tests, [3]
 // div_rn bad, [4] sqrt_fast tests, [5] sqrt_fast bad, [6] compiler sqrt bad, [7]
@@ -414,6 +416,12 @@ __global__ void __launch_bounds__(256) k_selftest_math(uint32_t n, uint32_t seed
     const bool acc = st_accept(ref);
     bad_d += (acc != st_accept(q) || (acc && !st_same(q, ref))) ? 1u : 0u;
     bad_dc += st_same(nn / dd, ref) ? 0u : 1u;
+    // Moller-Trumbore's 1/det (mt_test<true>): every det the render limits admit past
+    // the |det| >= 1e-12 rejection, 2^-40 <= |det| < 2^95, must give the IEEE bits
+    const float det = st_float(st_hash(h2 ^ 0x2545f491u), 127u - 40u, 127u + 94u);
+    const float rref = (float)(1.0 / (double)det);
+    bad_d += st_same(div_rn(1.0f, det), rref) ? 0u : 1u;
+    bad_dc += st_same(1.0f / det, rref) ? 0u : 1u;
   }
   atomicAdd(&counts[1], (unsigned long long)bad_s);
   atomicAdd(&counts[3], (unsigned long long)bad_d);

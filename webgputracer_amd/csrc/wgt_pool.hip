@@ -99,7 +99,8 @@ __device__ __forceinline__ uint32_t lowest_bits(uint32_t mask, uint32_t m) {
   return mask & ((1u << nth_set_bit(mask, m)) - 1u);
 }
 
-// Ray record, 4 x float4: (o, bt), (d, bi), (inv, ref | sp << 23), (ot, lf/64 | (le-lf)/64 << 20 | col << 24).
+// Ray record, 4 x float4: (o, bt), (d, bi), (inv, ref | sp << 23), (ot, triangle | count << 20 | col << 24)
+// (the open leaf's next triangle and the triangles left in it, in records of kTriRecordBytes).
 // Exact for Stack24 trees: internal refs are byte offsets < 2^23 (kNoRef coded 0x7fffff,
 // never a multiple of 80 or 128), sp <= 32, triangles < 2^20, a leaf <= 8 triangles,
 // stack columns < 256.
@@ -110,7 +111,8 @@ __device__ __forceinline__ void rec_put(float4* __restrict__ r, f3 o, f3 d, cons
   r[1] = make_float4(d.x, d.y, d.z, __uint_as_float(t.bi));
   r[2] = make_float4(t.inv.x, t.inv.y, t.inv.z, __uint_as_float(ref | ((uint32_t)t.sp << 23)));
   r[3] = make_float4(t.ot.x, t.ot.y, t.ot.z,
-                     __uint_as_float((t.lf >> 6) | (((t.le - t.lf) >> 6) << 20) | (col << 24)));
+                     __uint_as_float((t.lf / kTriRecordBytes) | (((t.le - t.lf) / kTriRecordBytes) << 20) |
+                                     (col << 24)));
 }
 __device__ __forceinline__ void rec_get(const float4* __restrict__ r, f3& o, f3& d, Trav& t, uint32_t& col) {
   const float4 a = r[0], b = r[1], c = r[2], e = r[3];
@@ -124,8 +126,8 @@ __device__ __forceinline__ void rec_get(const float4* __restrict__ r, f3& o, f3&
   const uint32_t ref = w2 & kRecNoRef;
   t.ref = ref == kRecNoRef ? kNoRef : (int)ref;
   t.sp = (int)(w2 >> 23);
-  t.lf = (w3 & 0xfffffu) << 6;
-  t.le = t.lf + (((w3 >> 20) & 0xfu) << 6);
+  t.lf = (w3 & 0xfffffu) * kTriRecordBytes;
+  t.le = t.lf + ((w3 >> 20) & 0xfu) * kTriRecordBytes;
   col = w3 >> 24;
 }
 
@@ -303,7 +305,7 @@ k_render_pool(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, ucha
           trav_init<CN>(sc, ro, rd, q_prim != kNoHit, q_t, t);
           stk.col = threadIdx.x;
           hticket = -1;
-          node_step<STATS, CN>(sc, t, stk, st);  // the root: rays that miss it never traverse
+          root_step<STATS, CN>(sc, t, stk, st);  // the root: rays that miss it never traverse
           if (trav_done(t)) pend = true;
           else hold = true;
           break;

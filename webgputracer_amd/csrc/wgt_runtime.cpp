@@ -216,10 +216,12 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
 // Numeric limits under which the kernels' short division (wgt_math.h div_rn, the
 // quad plane distance) is exact wherever it decides anything:
 // scene coordinates and ray origins within 2^40, quad normals within 2 per
-// component (or NaN: a degenerate quad), primary ray directions within 2^32
+// component (or NaN: a degenerate quad), triangle edge components within 2^30 (the
+// short 1/det of Moller-Trumbore), primary ray directions within 2^32
 // (scattered directions are unit).  Everything else in the kernels is exact for
 // any input.  Outside the limits the calls fail with WGT_E_INVALID.
 constexpr double kCoordLimit = 1099511627776.0;  // 2^40
+constexpr double kEdgeLimit = 1073741824.0;      // 2^30: triangle edges (Moller-Trumbore's short 1/det)
 constexpr double kPrimaryDirLimit = 4294967296.0;  // 2^32
 
 bool finite_within(const float* v, int n, double lim) {
@@ -242,10 +244,14 @@ std::string check_scene_limits(const wgt_quad* lq, uint32_t nlq, const wgt_spher
   for (uint32_t i = 0; i < ns; ++i)
     if (!finite_within(sp[i].center, 3, kCoordLimit) || !finite_within(&sp[i].radius, 1, kCoordLimit))
       return "sphere " + std::to_string(i) + ": center and radius must be finite and within 2^40";
-  for (uint32_t i = 0; i < nt; ++i)
+  for (uint32_t i = 0; i < nt; ++i) {
     if (!finite_within(tr[i].v0, 3, kCoordLimit) || !finite_within(tr[i].e1, 3, kCoordLimit) ||
         !finite_within(tr[i].e2, 3, kCoordLimit))
       return "triangle " + std::to_string(i) + ": vertices must be finite and within 2^40";
+    // |det| <= |e1| |e2| |d| < 3 * 2^60 * 2^32 < 2^94: mt_test's short 1/det is exact
+    if (!finite_within(tr[i].e1, 3, kEdgeLimit) || !finite_within(tr[i].e2, 3, kEdgeLimit))
+      return "triangle " + std::to_string(i) + ": edge components must be within 2^30";
+  }
   return "";
 }
 
@@ -640,7 +646,22 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
       std::memcpy(&bvh.nodes[i * kNode4Floats + 24 + k], &r128, 4);
     }
   const size_t b_cnodes = align256(crec.size() * 4);
-  const size_t b_tris = align256(bvh.tris.size() * 4);
+  // the device triangle records (wgt_geom.h kTriRecordBytes): the builder's 64-B records,
+  // or their 40-B form without the padded box
+  std::vector<float> dtris;
+  if (kTriRecordBytes == 64) {
+    dtris = bvh.tris;
+  } else {
+    dtris.resize((size_t)n_tris * (kTriRecordBytes / 4));
+    for (size_t i = 0; i < n_tris; ++i) {
+      const float* a = &bvh.tris[i * kTriRecordFloats];
+      float* o = &dtris[i * (kTriRecordBytes / 4)];
+      o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3];     // v0, index bits
+      o[4] = a[4]; o[5] = a[5]; o[6] = a[6];                  // e1
+      o[7] = a[8]; o[8] = a[9]; o[9] = a[10];                 // e2
+    }
+  }
+  const size_t b_tris = align256(dtris.size() * 4);
   const size_t b_shade = align256(bvh.tshade.size() * 4);
   const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes;
 
@@ -661,7 +682,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   std::memcpy(host.data() + b_quads, spheres, (size_t)n_spheres * 32);
   if (n_tris) {
     std::memcpy(host.data() + b_quads + b_sph, bvh.nodes.data(), bvh.nodes.size() * 4);
-    std::memcpy(host.data() + b_quads + b_sph + b_nodes, bvh.tris.data(), bvh.tris.size() * 4);
+    std::memcpy(host.data() + b_quads + b_sph + b_nodes, dtris.data(), dtris.size() * 4);
     std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris, bvh.tshade.data(),
                 bvh.tshade.size() * 4);
     std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade, crec.data(), crec.size() * 4);
@@ -913,7 +934,7 @@ int wgt_selftest_math(wgt_ctx* ctx, uint32_t n, uint32_t seed, uint64_t counts[8
   WGT_HIP(ctx, hipMemcpyAsync(counts, ctx->prim.p, 64, hipMemcpyDeviceToHost, ctx->stream));
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   counts[0] = 1ull << 32;  // sqrt: every bit pattern
-  counts[2] = n;
+  counts[2] = 2ull * n;    // n quad-distance quotients + n Moller-Trumbore reciprocals
   return WGT_OK;
 }
 
