@@ -469,15 +469,49 @@ __device__ __forceinline__ void root_step(const DevScene& sc, Trav& t, const STK
 template <bool STATS, bool CN = false, class STK>
 __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, const STK& lds,
                                          TravStats& st) {
+  // 1/d: under CN t.inv holds s/d, and (s/d) * (1/s) is 1/d exactly
+  const f3 inv = CN ? sc.rcstep * t.inv : t.inv;
+#if WGT_TRI_PER_STEP > 1
+  // up to WGT_TRI_PER_STEP triangles of the open leaf per step, their loads issued together
+  // (a slot past the leaf's end re-reads the first record and is ignored): the closest hit
+  // is a minimum over (t, index), so testing them against the same bound and merging is exact
+  constexpr int K = WGT_TRI_PER_STEP;
+  float tt[K];
+  uint32_t idx[K];
+  bool hit[K];
+  uint32_t n = 1;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    const uint32_t a = t.lf + uint32_t(j) * kTriRecordBytes;
+    const bool live = j == 0 || a < t.le;
+    hit[j] = tri_test<true>(sc, live ? a : t.lf, o, d, t.ot, inv, t.bt, t.bi, tt[j], idx[j]);
+    if (j > 0) {
+      hit[j] = hit[j] && live;
+      n += live ? 1u : 0u;
+    }
+  }
+  if (hit[0]) {  // passed tri_test's own (t, index) filter against the same bound
+    t.bt = tt[0];
+    t.bi = idx[0];
+  }
+#pragma unroll
+  for (int j = 1; j < K; ++j)
+    if (hit[j] && (tt[j] < t.bt || (tt[j] == t.bt && idx[j] < t.bi))) {
+      t.bt = tt[j];
+      t.bi = idx[j];
+    }
+  if (STATS) st.tris += n;
+  t.lf += n * kTriRecordBytes;
+#else
   if (STATS) st.tris++;
   float tt;
   uint32_t idx;
-  // 1/d: under CN t.inv holds s/d, and (s/d) * (1/s) is 1/d exactly
-  if (tri_test<true>(sc, t.lf, o, d, t.ot, CN ? sc.rcstep * t.inv : t.inv, t.bt, t.bi, tt, idx)) {
+  if (tri_test<true>(sc, t.lf, o, d, t.ot, inv, t.bt, t.bi, tt, idx)) {
     t.bt = tt;
     t.bi = idx;
   }
   t.lf += kTriRecordBytes;
+#endif
   if (t.lf >= t.le && t.ref == kNoRef) trav_resolve(sc, t, kNoRef, lds);
 }
 

@@ -106,6 +106,13 @@ constexpr int kTriRecordFloats = 16;  // the host / exported record (wgt_bvh_bui
 #endif
 static_assert(WGT_TRI_REC == 64 || WGT_TRI_REC == 40, "triangle record: 64 or 40 bytes");
 constexpr uint32_t kTriRecordBytes = WGT_TRI_REC;
+// triangles tested per triangle step of the phase-split kernel (wgt_device.h tri_step): two
+// measured -1.6% on sponza, -1.3% on bunny at 1080p/256 spp; three and four +6%/+13% on sponza
+// (profiles/sweeps/r03_ab_tri_per_step.log)
+#ifndef WGT_TRI_PER_STEP
+#define WGT_TRI_PER_STEP 2
+#endif
+static_assert(WGT_TRI_PER_STEP >= 1 && WGT_TRI_PER_STEP <= 4, "1 to 4 triangles per step");
 
 // BVH4 node, 128 B (8 x float4, one L2 cache line), children in SoA order:
 //   N[0] = lo.x of children 0..3   N[1] = hi.x   N[2] = lo.y   N[3] = hi.y
