@@ -543,10 +543,57 @@ void CompactNode(const float* n, float s, double G, uint32_t* q) {
   q[3] = 0u;  // reserved
 }
 
+// The 64-B compact form (wgt_geom.h, WGT_CN64): the same codes, relative to an origin on a
+// grid of 512 steps, org/s = 512 K with K a signed byte (stored beside the refs).  q: 16 words,
+// the x, y, z code words (as CompactNode's q[4..15]), then four words whose top bytes hold K
+// for x, y, z and 0 (the upload ORs the 24-bit refs into their low bytes).  false when some
+// K is outside [-128, 127] (the scene lies too far from the world origin for this form).
+bool CompactNode64(const float* n, float s, double G, uint32_t* q) {
+  bool live[kBvhWidth];
+  for (int i = 0; i < kBvhWidth; ++i) live[i] = !(n[i] == kEmptySlotCoord && n[4 + i] == kEmptySlotCoord);
+  bool ok = true;
+  for (int a = 0; a < 3; ++a) {
+    double ulo = std::numeric_limits<double>::infinity();
+    for (int i = 0; i < kBvhWidth; ++i)
+      if (live[i]) ulo = std::min(ulo, (double)n[(2 * a) * 4 + i]);
+    const double K = std::floor((ulo - G) / (double)s / 512.0);
+    if (!(K >= -128.0 && K <= 127.0)) ok = false;
+    const double orgd = 512.0 * std::min(std::max(K, -128.0), 127.0) * (double)s;
+    uint32_t lo_h[kBvhWidth], hi_h[kBvhWidth];
+    for (int i = 0; i < kBvhWidth; ++i) {
+      lo_h[i] = hi_h[i] = 0x7c00u;
+      if (!live[i]) continue;
+      const double blo = (double)n[(2 * a) * 4 + i] - G, bhi = (double)n[(2 * a + 1) * 4 + i] + G;
+      uint32_t l = 0, r = 0x7bffu;
+      while (l < r) {
+        const uint32_t m = (l + r + 1) / 2;
+        if (CDecD(m, s, orgd) <= blo) l = m; else r = m - 1;
+      }
+      lo_h[i] = l;
+      l = 0; r = 0x7bffu;
+      while (l < r) {
+        const uint32_t m = (l + r) / 2;
+        if (CDecD(m, s, orgd) >= bhi) r = m; else l = m + 1;
+      }
+      hi_h[i] = l;
+      if (CDecD(lo_h[i], s, orgd) > blo || CDecD(hi_h[i], s, orgd) < bhi) ok = false;
+    }
+    q[4 * a + 0] = lo_h[0] | (lo_h[1] << 16);
+    q[4 * a + 1] = lo_h[2] | (lo_h[3] << 16);
+    q[4 * a + 2] = hi_h[0] | (hi_h[1] << 16);
+    q[4 * a + 3] = hi_h[2] | (hi_h[3] << 16);
+    q[12 + a] = (uint32_t)(uint8_t)(int8_t)std::min(std::max(K, -128.0), 127.0) << 24;
+  }
+  q[15] = 0u;
+  return ok;
+}
+
 // The smallest power-of-two step with which code 65504 reaches every node's upper
 // bounds plus the margins (the origin sits up to G + one float step of org/s below
 // the lower bound).
-float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes, double G) {
+// gap: how far below the lower bound (minus G) the origin may sit, in steps (0: the float
+// org/s of CompactNode; 512: the grid origin of CompactNode64)
+float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes, double G, double gap = 0.0) {
   int e = -24;
   for (;;) {
     const float s = std::ldexp(1.0f, e);
@@ -560,7 +607,7 @@ float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes, double G) {
             ulo = std::min(ulo, (double)n[(2 * a) * 4 + i]);
             uhi = std::max(uhi, (double)n[(2 * a + 1) * 4 + i]);
           }
-        const double org_low = ulo - G - (std::fabs(ulo - G) * 0x1p-23 + (double)s * 0x1p-126);
+        const double org_low = ulo - G - (std::fabs(ulo - G) * 0x1p-23 + (double)s * 0x1p-126) - gap * (double)s;
         ok = org_low + 65504.0 * (double)s >= uhi + G;
       }
     }
@@ -698,6 +745,11 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
     CompactNode(&out.nodes[(size_t)i * kNode4Floats], out.cstep, G, &out.cnodes[(size_t)i * kCNodeFloats]);
     std::memcpy(&out.crefs[(size_t)i * 4], &out.nodes[(size_t)i * kNode4Floats + 24], 16);
   }
+  out.c64step = CompactStep(out.nodes, out.n_nodes, G, 512.0);
+  out.c64.resize((size_t)out.n_nodes * 16);
+  out.c64_ok = true;
+  for (uint32_t i = 0; i < out.n_nodes; ++i)
+    out.c64_ok &= CompactNode64(&out.nodes[(size_t)i * kNode4Floats], out.c64step, G, &out.c64[(size_t)i * 16]);
   out.tris.resize((size_t)n * kTriRecordFloats);
   for (uint32_t i = 0; i < n; ++i) {
     const wgt_triangle& t = tris[prims[i].idx];

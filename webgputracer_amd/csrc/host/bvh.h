@@ -17,6 +17,9 @@ struct BvhOut {
   std::vector<int32_t> crefs;    // 4 child refs per node (the compact form's ref records)
   float cstep = 1.0f;            // scene-wide decode step of the compact nodes
   float cbound = 0.0f;           // M: the compact codes are exact for ray origins with |o| <= M
+  std::vector<uint32_t> c64;     // 16 words per node: the 64-B compact form without refs (WGT_CN64)
+  float c64step = 1.0f;          // its decode step
+  bool c64_ok = false;           // every node's grid origin fits a signed byte
   std::vector<float> tris;    // kTriRecordFloats per triangle, leaf order (wgt_geom.h)
   std::vector<float> tshade;  // 8 floats per original triangle
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;  // BVH4 nodes / depth

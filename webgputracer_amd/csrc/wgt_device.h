@@ -263,10 +263,20 @@ __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int
                                           uint32_t& k2, uint32_t& k3, int& r0, int& r1, int& r2, int& r3) {
   if (CN) {
     const float4* __restrict__ n = (const float4*)((const char*)sc.cnodes + (uint32_t)ref);  // ref: byte offset
+#ifdef WGT_CN64
+    const uint4 x = __builtin_bit_cast(uint4, n[0]), y = __builtin_bit_cast(uint4, n[1]),
+                z = __builtin_bit_cast(uint4, n[2]), w = __builtin_bit_cast(uint4, n[3]);
+    const int4 rf = int4{__builtin_amdgcn_sbfe((int)w.x, 0, 24), __builtin_amdgcn_sbfe((int)w.y, 0, 24),
+                         __builtin_amdgcn_sbfe((int)w.z, 0, 24), __builtin_amdgcn_sbfe((int)w.w, 0, 24)};
+    // org/s = 512 K, K the signed top byte: exact
+    const float4 a = float4{__builtin_ldexpf((float)((int)w.x >> 24), 9), __builtin_ldexpf((float)((int)w.y >> 24), 9),
+                            __builtin_ldexpf((float)((int)w.z >> 24), 9), 0.0f};
+#else
     const int4 rf = __builtin_bit_cast(int4, n[4]);
     const float4 a = n[0];
     const uint4 x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]),
                 z = __builtin_bit_cast(uint4, n[3]);
+#endif
     // c = the slab distance of the node origin org' = (org/s) * s: fma(org/s, s/d, ot)
     const f3 c = f3{__builtin_fmaf(a.x, t.inv.x, t.ot.x), __builtin_fmaf(a.y, t.inv.y, t.ot.y),
                     __builtin_fmaf(a.z, t.inv.z, t.ot.z)};

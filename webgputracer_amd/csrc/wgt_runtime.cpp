@@ -630,6 +630,21 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const size_t b_nodes = align256(bvh.nodes.size() * 4);
   // compact records: the 64-B node followed by its 16-B refs (wgt_geom.h)
   std::vector<uint32_t> crec((size_t)bvh.n_nodes * kCRecordFloat4s * 4);
+#ifdef WGT_CN64
+  // the 64-B form: codes, then 24-bit refs (internal: byte offsets) under the origin bytes
+  bool c64 = bvh.c64_ok;
+  for (size_t i = 0; i < bvh.n_nodes; ++i) {
+    std::memcpy(&crec[i * 16], &bvh.c64[i * 16], 64);
+    for (int k = 0; k < 4; ++k) {
+      int64_t r = bvh.crefs[i * 4 + k];
+      if (r >= 0) r *= 64;
+      if (r >= (1 << 23) || r < -(1 << 23)) c64 = false;
+      crec[i * 16 + 12 + k] |= (uint32_t)r & 0xffffffu;
+    }
+  }
+  for (size_t i = 0; i < bvh.n_nodes; ++i)
+    for (int k = 0; k < 4; ++k) {
+#else
   for (size_t i = 0; i < bvh.n_nodes; ++i) {
     std::memcpy(&crec[i * kCRecordFloat4s * 4], &bvh.cnodes[i * kCNodeFloats], kCNodeFloats * 4);
     std::memcpy(&crec[i * kCRecordFloat4s * 4 + kCNodeFloats], &bvh.crefs[i * 4], 16);
@@ -640,6 +655,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     for (int k = 0; k < 4; ++k) {
       int32_t& r = reinterpret_cast<int32_t&>(crec[i * kCRecordFloat4s * 4 + kCNodeFloats + k]);
       if (r >= 0) r *= (int32_t)(kCRecordFloat4s * 16);
+#endif
       int32_t r128;
       std::memcpy(&r128, &bvh.nodes[i * kNode4Floats + 24 + k], 4);
       if (r128 >= 0) r128 *= (int32_t)(kNode4Floats * 4);
@@ -697,9 +713,14 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.tris = (const float4*)(base + b_quads + b_sph + b_nodes);
   sc.tshade = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris);
   sc.cnodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade);
+#ifdef WGT_CN64
+  sc.cstep = bvh.c64step;
+  sc.cbound = c64 ? bvh.cbound : -1.0f;  // a tree the 64-B form cannot hold reads the 128-B nodes
+#else
   sc.cstep = bvh.cstep;
-  sc.rcstep = 1.0f / bvh.cstep;  // a power of two: exact
   sc.cbound = bvh.cbound;
+#endif
+  sc.rcstep = 1.0f / sc.cstep;  // a power of two: exact
   sc.n_lights = n_lights;
   sc.n_quads = n_quads;
   sc.n_spheres = n_spheres;
