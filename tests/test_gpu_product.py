@@ -271,3 +271,30 @@ def test_bench_two_ranks_self_checks(tmp_path):
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["check_frames_bit_exact"] is True
     assert line["check"]["world_size"] == 2 and line["check"]["frames"] == 2
+
+
+def test_bench_line_contract(tmp_path):
+    """bench.py at N = 1 on a small workload prints one JSON line with every field of the driver's
+    contract: throughput, timing, roofline (bound, achieved, peak, frac, traffic) and the CPU
+    baseline (value, unit, cores, kind, sample), plus the build id its traffic is keyed to."""
+    import json
+
+    cmd = [sys.executable, "bench.py", "--scene", "bunny", "--width", "96", "--height", "64", "--spp", "4",
+           "--steps", "2", "--warmup", "1", "--cpu-rows", "2", "--stats-reps", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "build_id"):
+        assert k in line, k
+    assert line["n_gpus"] == 1 and line["steps"] == 2 and line["warmup"] == 1 and line["value"] > 0
+    assert line["unit"] == "Mrays/s" and line["higher_is_better"] is True and line["dtype"] == "f32"
+    assert line["config"]["workload"] == "bunny-96x64-4spp"
+    rf = line["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] > 0
+    assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    assert "traffic" in rf  # null here: no profile entry for this workload
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"]
