@@ -214,6 +214,20 @@ def test_bunny_render_parity(ctx, wgt, oracle, bunny, W, H, spp, seed):
     check_counters(g["stats"], r["counters"], oracle)
 
 
+@pytest.mark.parametrize("W,H", [(1, 1), (1, 9), (9, 1), (7, 5), (65, 3)])
+def test_tiny_and_ragged_mesh_frames(ctx, wgt, oracle, bunny, W, H):
+    """Frames smaller than one 8x8 pixel block, or one block wide and ragged, through the
+    persistent mesh kernel (a grid of one or a few waves, most lanes without a pixel, the
+    cost pre-pass and LPT order over 1-9 blocks) against the oracle."""
+    (L, Q, S, T), osc = bunny
+    ctx.upload_scene(L, Q, S, T)
+    g = ctx.render_tile(wgt.camera_param(W / H, 9, 4), W, H, stats=True)
+    r = osc.render(oracle.camera_param(W / H, 9, 4), W, H)
+    assert_radiance(g["f32"], r["f32"])
+    assert np.array_equal(g["hit"], r["hit"])
+    check_counters(g["stats"], r["counters"], oracle)
+
+
 def test_bunny_1080p_256spp_subsample(ctx, wgt, oracle, bunny):
     """BASELINE config 3 at full size: GPU tiles of the 1920x1080/256spp frame vs the
     oracle on the same global pixels."""
