@@ -88,10 +88,70 @@ def parse():
     p.add_argument("--pipeline", type=int, default=2,
                    help="frames in flight: step k runs on the context's pipeline stream k %% P, so the next "
                         "frame fills the CUs the previous frame's end-of-launch drain leaves idle (1 = serial)")
+    p.add_argument("--pmc", default="auto", choices=["auto", "on", "off"],
+                   help="after the timed region, measure the dominant kernel's HBM traffic and L2 requests with "
+                        "separate rocprofv3 --pmc passes of one frame of this workload (child runs of this script); "
+                        "auto: at N = 1 when rocprofv3 is on PATH.  Failing that, the build-id-keyed profile entry")
     p.add_argument("--check", default="auto", choices=["auto", "on", "off"],
                    help="one untimed step before timing whose gathered frames rank 0 compares bit for bit with "
                         "single-launch renders of the same seeds (auto: on when N > 1)")
     return p.parse_args()
+
+
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",), ("TCC_HIT_sum", "TCC_MISS_sum"))
+
+
+def live_pmc(args, kernel):
+    """HBM bytes and L2 requests per launch of `kernel`, measured now on this device and binary:
+    one rocprofv3 --pmc pass per counter group (never combined with traces; each pass within the
+    per-block counter limits, under its own kill timeout) over a child run of this script that
+    renders one frame of the same workload alone.  HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x
+    1 KiB (FETCH_SIZE counts half the bytes of 16-B-per-lane reads on gfx950, MI355X_MICROARCH.md
+    §HBM).  Returns (result dict, note); the dict is None when a pass fails."""
+    import csv
+    import shutil
+    import subprocess
+    import tempfile
+
+    prof = shutil.which("rocprofv3")
+    if prof is None:
+        return None, "rocprofv3 not on PATH"
+    child = [sys.executable, os.path.abspath(__file__), "--scene", args.scene, "--width", str(args.width),
+             "--height", str(args.height), "--spp", str(args.spp), "--tile", str(args.tile), "--steps", "1",
+             "--warmup", "0", "--pipeline", "1", "--no-cpu-baseline", "--check", "off", "--pmc", "off",
+             "--stats-reps", "1"]
+    agg, calls = {}, 0
+    for ctrs in PMC_PASSES:
+        d = tempfile.mkdtemp(prefix="wgt_pmc_")
+        cmd = ["timeout", "-s", "KILL", "300", prof, "--pmc", *ctrs, "-d", d, "-o", "run", "--output-format", "csv",
+               "--", *child]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=330, cwd=ROOT)
+            rows = []
+            for root, _, files in os.walk(d):
+                for fn in files:
+                    if fn.endswith("counter_collection.csv"):
+                        with open(os.path.join(root, fn)) as f:
+                            rows += list(csv.DictReader(f))
+            if r.returncode != 0 or not rows:
+                return None, f"rocprofv3 --pmc {' '.join(ctrs)} failed (exit {r.returncode})"
+            disp = set()
+            for row in rows:
+                if kernel in row["Kernel_Name"]:
+                    agg[row["Counter_Name"]] = agg.get(row["Counter_Name"], 0.0) + float(row["Counter_Value"])
+                    disp.add(row["Dispatch_Id"])
+            if not disp:
+                return None, f"no dispatch of {kernel} in the --pmc {' '.join(ctrs)} pass"
+            calls = len(disp)
+        except (OSError, subprocess.SubprocessError, KeyError, ValueError) as e:
+            return None, f"rocprofv3 pass failed: {e}"
+        finally:
+            shutil.rmtree(d, ignore_errors=True)
+    hbm = (2.0 * agg.get("FETCH_SIZE", 0.0) + agg.get("WRITE_SIZE", 0.0)) * 1024.0 / calls
+    req = (agg.get("TCC_HIT_sum", 0.0) + agg.get("TCC_MISS_sum", 0.0)) / calls
+    hit = agg.get("TCC_HIT_sum", 0.0) / max(agg.get("TCC_HIT_sum", 0.0) + agg.get("TCC_MISS_sum", 0.0), 1.0)
+    return {"hbm_bytes_per_launch": hbm, "tcc_requests_per_launch": req, "tcc_hit_rate": round(hit, 4)}, \
+        f"live: {len(PMC_PASSES)} rocprofv3 --pmc passes of one frame of this workload alone, this run"
 
 
 def build_scene(w, kind):
@@ -325,6 +385,23 @@ def main():
                           "calibration": os.path.relpath(L2_CALIB_JSON, ROOT)}
         except (OSError, ValueError, KeyError):
             pass
+        # live PMC passes of this binary on this device (N = 1), in place of the profile entry
+        traffic_source = "profile" if traffic is not None else None
+        if world == 1 and (args.pmc == "on" or (args.pmc == "auto" and args.steps > 0)):
+            live, note = live_pmc(args, kernel)
+            if live is not None:
+                traffic, tj_id, traffic_note, traffic_source = live["hbm_bytes_per_launch"], build_id, note, "live"
+                req = live["tcc_requests_per_launch"]
+                with open(L2_CALIB_JSON) as f:
+                    bpr = json.load(f)["bytes_per_request"]
+                if req and kern_ms > 0:
+                    l2_gbs = req * bpr / (kern_ms * 1e-3) / 1e9
+                    l2 = {"requests_per_launch": req, "bytes_per_request": bpr, "achieved": round(l2_gbs, 1),
+                          "peak": L2_PEAK_GBS, "unit": "GB/s", "frac": round(l2_gbs / L2_PEAK_GBS, 4),
+                          "hit_rate": live["tcc_hit_rate"], "source": "live rocprofv3 --pmc passes",
+                          "calibration": os.path.relpath(L2_CALIB_JSON, ROOT)}
+            else:
+                traffic_note = f"{note}; {traffic_note}"
         nodes = [int(x["node_visits"]) for x in sts]
         tris = [int(x["tri_tests"]) for x in sts]
         n_tris = info["n_tris"]
@@ -365,7 +442,7 @@ def main():
                          else 0.0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(survey_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if kern_ms > 0
                          else 0.0, "traffic": traffic, "traffic_build_id": tj_id if traffic is not None else None,
-                         "traffic_note": traffic_note,
+                         "traffic_source": traffic_source, "traffic_note": traffic_note,
                          "bytes_per_unit": {"node": SURVEY_NODE_BYTES, "tri": SURVEY_TRI_BYTES,
                                             "shade_per_ray": SHADE_BYTES},
                          # the bytes this implementation's encodings load per launch (80-B compact or 112-B

@@ -275,8 +275,9 @@ def test_bench_two_ranks_self_checks(tmp_path):
 
 def test_bench_line_contract(tmp_path):
     """bench.py at N = 1 on a small workload prints one JSON line with every field of the driver's
-    contract: throughput, timing, roofline (bound, achieved, peak, frac, traffic) and the CPU
-    baseline (value, unit, cores, kind, sample), plus the build id its traffic is keyed to."""
+    contract: throughput, timing, roofline (bound, achieved, peak, frac, traffic measured by the
+    run's own rocprofv3 --pmc passes) and the CPU baseline (value, unit, cores, kind, sample),
+    plus the build id."""
     import json
 
     cmd = [sys.executable, "bench.py", "--scene", "bunny", "--width", "96", "--height", "64", "--spp", "4",
@@ -295,6 +296,8 @@ def test_bench_line_contract(tmp_path):
     rf = line["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] > 0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
-    assert "traffic" in rf  # null here: no profile entry for this workload
+    # measured live by the run's own rocprofv3 --pmc passes (no profile entry exists for this workload)
+    assert rf["traffic_source"] == "live" and rf["traffic"] > 0 and rf["traffic_build_id"] == line["build_id"]
+    assert rf["l2"]["requests_per_launch"] > 0 and 0.0 <= rf["l2"]["hit_rate"] <= 1.0
     cb = line["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"]
