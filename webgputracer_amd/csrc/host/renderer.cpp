@@ -11,6 +11,8 @@
 #include <iomanip>
 #include <iostream>
 #include <sstream>
+#include <thread>
+#include <vector>
 
 #include "procedural.h"
 
@@ -108,15 +110,21 @@ bool Renderer::OnRenderBatch(uint32_t first, uint32_t n) {
     std::cerr << "[WebGPUTracer] render failed: " << wgt_last_error(ctx_) << std::endl;
     return false;
   }
-  for (uint32_t j = 0; j < n; ++j) {
-    std::ostringstream sout;
-    sout << std::setw(3) << std::setfill('0') << first + j;
-    if (cfg_.write_png) {
-      std::string output_file = cfg_.out_dir + "/" + sout.str() + ".png";
-      if (wgt_write_png(output_file.c_str(), images.data() + frame_bytes * j, cfg_.width, cfg_.height) != WGT_OK) {
-        std::cerr << "[WebGPUTracer] Image output failed." << std::endl;
-        return false;
-      }
+  if (cfg_.write_png) {  // the batch's PNGs are encoded concurrently, one thread per frame
+    std::vector<int> rc(n, WGT_OK);
+    std::vector<std::thread> writers;
+    for (uint32_t j = 0; j < n; ++j) {
+      writers.emplace_back([&, j] {
+        std::ostringstream sout;
+        sout << std::setw(3) << std::setfill('0') << first + j;
+        const std::string output_file = cfg_.out_dir + "/" + sout.str() + ".png";
+        rc[j] = wgt_write_png(output_file.c_str(), images.data() + frame_bytes * j, cfg_.width, cfg_.height);
+      });
+    }
+    for (auto& t : writers) t.join();
+    if (std::any_of(rc.begin(), rc.end(), [](int r) { return r != WGT_OK; })) {
+      std::cerr << "[WebGPUTracer] Image output failed." << std::endl;
+      return false;
     }
   }
   image_.assign(images.end() - frame_bytes, images.end());

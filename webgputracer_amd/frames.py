@@ -26,9 +26,11 @@ single-frame render.
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import os
 import time
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 
@@ -47,6 +49,13 @@ def frames_of_rank(start: int, end: int, rank: int, world: int):
     """Frame indices of `--frame start end` (frame_indices) dealt to `rank`:
     round-robin, as even as the range allows."""
     return [f for k, f in enumerate(frame_indices(start, end)) if k % world == rank]
+
+
+def _cpu_share() -> int:
+    """CPUs this process may use, capped by OMP_NUM_THREADS where the launcher sets it."""
+    n = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(n, omp) if omp > 0 else n
 
 
 def batches(frames, batch: int):
@@ -126,6 +135,8 @@ def main(argv=None):
                          "profiles/configs/r02_c5_frames.jsonl)")
     ap.add_argument("--pipeline", type=int, default=2, help="batches in flight (1..4, DESIGN.md §4.2a)")
     ap.add_argument("--out", default=None, help="directory for NNN.png (none: render only)")
+    ap.add_argument("--png-threads", type=int, default=0,
+                    help="PNG encoder threads (0: this process's CPU share, capped by OMP_NUM_THREADS)")
     a = ap.parse_args(argv)
     if a.frame[0] < 1 or a.frame[1] < a.frame[0]:
         ap.error("bad frame range")  # the C++ CLI's check (csrc/main.cpp)
@@ -152,12 +163,24 @@ def main(argv=None):
     mine = frames_of_rank(a.frame[0], a.frame[1], rank, world)
     if a.out:
         os.makedirs(a.out, exist_ok=True)
+    # PNG encoding (zlib on the host, ~0.5 s per 1080p frame) runs on a thread pool while the GPU
+    # renders the next batches (wgt_write_png is a ctypes call: it releases the GIL); at most
+    # 4 frames per writer are held
+    workers = max(1, a.png_threads or _cpu_share())
+    pool = ThreadPoolExecutor(max_workers=workers) if a.out else None
+    pending = collections.deque()
     t0 = time.perf_counter()
     for b, imgs in fr.stream(batches(mine, a.batch), depth=a.pipeline):
         if a.out:
-            for f in b:
-                write_png(os.path.join(a.out, f"{f:03d}.png"), imgs[f])  # render.cpp:494-497
+            for f in b:  # render.cpp:494-497
+                pending.append(pool.submit(write_png, os.path.join(a.out, f"{f:03d}.png"), imgs[f]))
+            while len(pending) > 4 * workers:
+                pending.popleft().result()
+    while pending:
+        pending.popleft().result()
     dt = time.perf_counter() - t0
+    if pool:
+        pool.shutdown()
     torch.cuda.synchronize()
     print(json.dumps({"rank": rank, "world": world, "frames": len(mine), "batch": a.batch, "pipeline": a.pipeline,
                       "seconds": round(dt, 3),
