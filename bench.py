@@ -123,10 +123,12 @@ def live_pmc(args, kernel):
     agg, calls = {}, 0
     for ctrs in PMC_PASSES:
         d = tempfile.mkdtemp(prefix="wgt_pmc_")
-        cmd = ["timeout", "-s", "KILL", "300", prof, "--pmc", *ctrs, "-d", d, "-o", "run", "--output-format", "csv",
+        # a pass takes ~10-20 s (child start, scene build, one frame); a stuck one is killed, and the
+        # first failure ends the measurement (the remaining passes are not tried)
+        cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", *ctrs, "-d", d, "-o", "run", "--output-format", "csv",
                "--", *child]
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=330, cwd=ROOT)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=ROOT)
             rows = []
             for root, _, files in os.walk(d):
                 for fn in files:
