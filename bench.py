@@ -310,12 +310,16 @@ def main():
     barrier()
     t1 = time.perf_counter()
     elapsed = t1 - t0
-    # per-launch time: serial steps, the event pair around each launch; pipelined, the
-    # steady-state interval between consecutive launch completions (an event pair would
-    # also count the time a launch waits for the CUs its predecessor still holds)
+    # per-launch time: serial steps, the event pair around each launch; pipelined, the span
+    # from the first launch's start (on an idle device: the region starts synchronised) to the
+    # last launch's end over K launches.  An event pair would also count the time a launch
+    # waits for the CUs its predecessor holds, and the interval between the first and last
+    # completions is biased at small K: two frames in flight share the device and complete
+    # in pairs (3 steps: 158 ms "per launch" against 301 ms per step).  The span includes
+    # one fill and one drain, so it errs high (slower), by about 6% / K.
     spans = [a.elapsed_time(b) for a, b in evs]
     if P > 1 and args.steps > 1:
-        kern_ms = evs[0][1].elapsed_time(evs[-1][1]) / (args.steps - 1)
+        kern_ms = evs[0][0].elapsed_time(evs[-1][1]) / args.steps
     else:
         kern_ms = float(np.mean(spans)) if args.steps else 0.0
     # one more launch alone on an idle device (untimed): the single-frame latency
@@ -431,7 +435,7 @@ def main():
             "timing": {"pipeline": P,
                        "launch_ms": round(kern_ms, 3),
                        "launch_ms_is": "event pair around each launch" if P == 1 or args.steps < 2 else
-                       "steady-state interval between consecutive launch completions (HIP events; "
+                       "span from the first launch's start to the last launch's end / K (HIP events; "
                        f"{P} frames in flight on the context's pipeline streams)",
                        "isolated_launch_ms": round(iso, 3) if iso is not None else round(kern_ms, 3)},
             "simt_utilisation": {k: round(v, 4) for k, v in simt.items()},

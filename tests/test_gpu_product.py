@@ -296,6 +296,9 @@ def test_bench_line_contract(tmp_path):
     rf = line["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] > 0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # the per-launch time of pipelined frames cannot undercount the wall time per step at small K
+    # (the first-to-last completion interval did: two frames in flight complete in pairs)
+    assert line["kernel_ms"] <= line["ms_per_step"] * 1.001
     # measured live by the run's own rocprofv3 --pmc passes (no profile entry exists for this workload)
     assert rf["traffic_source"] == "live" and rf["traffic"] > 0 and rf["traffic_build_id"] == line["build_id"]
     assert rf["l2"]["requests_per_launch"] > 0 and 0.0 <= rf["l2"]["hit_rate"] <= 1.0
