@@ -304,3 +304,54 @@ def test_bench_line_contract(tmp_path):
     assert rf["l2"]["requests_per_launch"] > 0 and 0.0 <= rf["l2"]["hit_rate"] <= 1.0
     cb = line["cpu_baseline"]
     assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"]
+
+
+_RCCL_ONE_RANK = r"""
+import os, sys, json
+import numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["WGT_ROOT"])
+import webgputracer_amd as w
+from webgputracer_amd import dist as wdist
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm
+ctx = w.Context(0)
+ctx.upload_scene(*w.mesh_scene("bunny", target_tris=2000))
+W, H, T = 96, 64, 32
+cam = w.camera_param(W / H, 4, 0)
+sh = wdist.ShardedFrames(ctx, cam, W, H, T, [(0, 0)], 0, 1, dist, dev, backend="nccl")
+sh.launch(torch.cuda.current_stream().cuda_stream)
+buf = sh.bufs["u8"]
+# the collectives bench.py issues at N > 1, over RCCL: the tile gather to rank 0 and the
+# all_gather of the per-rank timing vector
+got = [torch.empty_like(buf)]
+dist.gather(buf, gather_list=got, dst=0)
+tv = torch.arange(7, dtype=torch.float64, device=dev)
+allv = [torch.zeros_like(tv)]
+dist.all_gather(allv, tv)
+torch.cuda.synchronize()
+img = sh.gather()["u8"][0].cpu().numpy()
+ref = ctx.render_tile(cam, W, H)["u8"]
+print(json.dumps({"backend": dist.get_backend(), "gather_equal": bool(torch.equal(got[0], buf)),
+                  "all_gather_equal": bool(torch.equal(allv[0], tv)),
+                  "frame_equal": bool(np.array_equal(img, ref))}))
+ctx.close()
+dist.destroy_process_group()
+"""
+
+
+def test_rccl_backend_one_rank(tmp_path):
+    """The RCCL ("nccl") backend initialises and runs bench.py's two collectives (the tile gather
+    to rank 0 and the all_gather of the timing vector) on this box's GPU, with one rank (RCCL
+    refuses two ranks on one device); the gathered tiles assemble to the single-launch frame.
+    The N > 1 RCCL runs themselves are the driver's (settings/run.py:11-24 is the reference's
+    multi-node analogue)."""
+    import json
+
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), WGT_ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", _RCCL_ONE_RANK], capture_output=True, text=True, timeout=240,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line == {"backend": "nccl", "gather_equal": True, "all_gather_equal": True, "frame_equal": True}, line
