@@ -52,12 +52,14 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the
 L2_CALIB_JSON = os.path.join(ROOT, "profiles", "l2_calibration.json")
 
 
-def dominant_kernel(compact: bool, waves: int, tris: bool = True) -> str:
-    """The timed k_render_ps instantiation <STATS, COST, compact nodes, waves per SIMD, triangles>
-    (a scene without triangles runs the 8-wave instantiation without traversal)."""
+def dominant_kernel(compact: bool, waves: int, tris: bool = True, park: bool = True) -> str:
+    """The timed k_render_ps instantiation <STATS, COST, compact nodes, waves per SIMD, triangles,
+    parked traversal state> (a scene without triangles runs the 8-wave instantiation without
+    traversal)."""
     if not tris:
-        return "wgt::k_render_ps<false, false, false, 8, false>"
-    return f"wgt::k_render_ps<false, false, {'true' if compact else 'false'}, {waves}, true>"
+        return "wgt::k_render_ps<false, false, false, 8, false, false>"
+    b = lambda x: "true" if x else "false"  # noqa: E731
+    return f"wgt::k_render_ps<false, false, {b(compact)}, {waves}, true, {b(park)}>"
 
 
 def compact_nodes(info) -> bool:
@@ -98,7 +100,45 @@ def parse():
     return p.parse_args()
 
 
-PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",), ("TCC_HIT_sum", "TCC_MISS_sum"))
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",), ("TCC_HIT_sum", "TCC_MISS_sum"),
+              ("SQ_WAVES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY",
+               "SQ_INSTS_VALU"))
+PMC_BUDGET_S = 180.0  # all live passes together (each also under its own kill timeout)
+N_SIMDS = 256 * 4     # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
+VALU_ISSUE_CYCLES = 2  # cycles of a wave64 f32 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md)
+
+
+def sq_fields(agg, calls):
+    """VALU-busy fraction and the wave-cycle split of the kernel from the SQ pass: waves are
+    issuing (SQ_ACTIVE_INST_ANY), parked in s_waitcnt (SQ_WAIT_ANY) or ready but not issued
+    (SQ_WAIT_INST_ANY); the three are disjoint and sum to SQ_WAVE_CYCLES (MI355X_MICROARCH.md
+    §rocprofv3).  A persistent launch keeps its waves for the whole launch, so the launch
+    lasts ~4 x SQ_WAVE_CYCLES / SQ_WAVES cycles (SQ_WAVE_CYCLES counts quad-cycles) and the
+    VALU pipes are busy SQ_INSTS_VALU x 2 cycles / (SIMDs x that)."""
+    wc = agg.get("SQ_WAVE_CYCLES", 0.0)
+    waves = agg.get("SQ_WAVES", 0.0)
+    if wc <= 0 or waves <= 0:
+        return None
+    launch_cycles = 4.0 * wc / waves
+    valu = agg.get("SQ_INSTS_VALU", 0.0) / calls
+    return {"valu_busy": round(valu * VALU_ISSUE_CYCLES / (N_SIMDS * launch_cycles), 4),
+            "valu_insts_per_launch": valu,
+            "wave_split": {"issuing": round(agg.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, 4),
+                           "waiting": round(agg.get("SQ_WAIT_ANY", 0.0) / wc, 4),
+                           "issue_stalled": round(agg.get("SQ_WAIT_INST_ANY", 0.0) / wc, 4)}}
+
+
+def limiter(hbm_frac, sq):
+    """What bounds the kernel, from the measurements: HBM bandwidth when the measured traffic
+    runs at >= 70 % of the peak, the VALU when its pipes are busy >= 70 % of the time, else the
+    latency of dependent memory round trips (waves parked in s_waitcnt) and VALU issue."""
+    if hbm_frac is not None and hbm_frac >= 0.7:
+        return "hbm"
+    if sq is not None and sq["valu_busy"] >= 0.7:
+        return "valu"
+    if sq is None:
+        return "unmeasured"
+    return "latency"
 
 
 def live_pmc(args, kernel):
@@ -121,14 +161,19 @@ def live_pmc(args, kernel):
              "--warmup", "0", "--pipeline", "1", "--no-cpu-baseline", "--check", "off", "--pmc", "off",
              "--stats-reps", "1"]
     agg, calls = {}, 0
+    t_end = time.monotonic() + PMC_BUDGET_S
     for ctrs in PMC_PASSES:
         d = tempfile.mkdtemp(prefix="wgt_pmc_")
-        # a pass takes ~10-20 s (child start, scene build, one frame); a stuck one is killed, and the
-        # first failure ends the measurement (the remaining passes are not tried)
-        cmd = ["timeout", "-s", "KILL", "150", prof, "--pmc", *ctrs, "-d", d, "-o", "run", "--output-format", "csv",
-               "--", *child]
+        # a pass takes ~10-20 s (child start, scene build, one frame); a stuck one is killed, the
+        # passes together stay within PMC_BUDGET_S, and the first failure ends the measurement
+        # (the remaining passes are not tried)
+        left = int(min(150.0, t_end - time.monotonic()))
+        if left < 20:
+            return None, f"live PMC passes exceeded their {PMC_BUDGET_S:.0f} s budget"
+        cmd = ["timeout", "-s", "KILL", str(left), prof, "--pmc", *ctrs, "-d", d, "-o", "run", "--output-format",
+               "csv", "--", *child]
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=180, cwd=ROOT)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=left + 30, cwd=ROOT)
             rows = []
             for root, _, files in os.walk(d):
                 for fn in files:
@@ -152,7 +197,8 @@ def live_pmc(args, kernel):
     hbm = (2.0 * agg.get("FETCH_SIZE", 0.0) + agg.get("WRITE_SIZE", 0.0)) * 1024.0 / calls
     req = (agg.get("TCC_HIT_sum", 0.0) + agg.get("TCC_MISS_sum", 0.0)) / calls
     hit = agg.get("TCC_HIT_sum", 0.0) / max(agg.get("TCC_HIT_sum", 0.0) + agg.get("TCC_MISS_sum", 0.0), 1.0)
-    return {"hbm_bytes_per_launch": hbm, "tcc_requests_per_launch": req, "tcc_hit_rate": round(hit, 4)}, \
+    return {"hbm_bytes_per_launch": hbm, "tcc_requests_per_launch": req, "tcc_hit_rate": round(hit, 4),
+            "write_bytes_per_launch": agg.get("WRITE_SIZE", 0.0) * 1024.0 / calls, "sq": sq_fields(agg, calls)}, \
         f"live: {len(PMC_PASSES)} rocprofv3 --pmc passes of one frame of this workload alone, this run"
 
 
@@ -284,6 +330,8 @@ def main():
             if ev is not None:
                 ev[1].record(s)
             got = shard.gather(slot=k % P)
+            if ev is not None:
+                ev[2].record(s)
         return got["u8"] if got is not None else None
 
     for k in range(args.warmup):
@@ -301,7 +349,9 @@ def main():
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # per step: launch start, launch end, gather end (the gather's time includes its wait for the
+    # slowest rank's tiles: where a multi-GPU step's efficiency goes)
+    evs = [tuple(torch.cuda.Event(enable_timing=True) for _ in range(3)) for _ in range(args.steps)]
     t0 = time.perf_counter()
     img = None
     for k in range(args.steps):
@@ -317,7 +367,8 @@ def main():
     # completions is biased at small K: two frames in flight share the device and complete
     # in pairs (3 steps: 158 ms "per launch" against 301 ms per step).  The span includes
     # one fill and one drain, so it errs high (slower), by about 6% / K.
-    spans = [a.elapsed_time(b) for a, b in evs]
+    spans = [a.elapsed_time(b) for a, b, _ in evs]
+    gather_ms = float(np.mean([b.elapsed_time(c) for _, b, c in evs])) if args.steps else 0.0
     if P > 1 and args.steps > 1:
         kern_ms = evs[0][0].elapsed_time(evs[-1][1]) / args.steps
     else:
@@ -335,7 +386,7 @@ def main():
         iso = e0.elapsed_time(e1)
 
     mine = np.array([elapsed, st["traced_rays"], st["queries"], st["samples"], st["node_visits"],
-                     st["tri_tests"], kern_ms], np.float64)
+                     st["tri_tests"], kern_ms, gather_ms, iso if iso is not None else kern_ms], np.float64)
     simt = {"path_loop": st["loop_lane_iters"] / max(64 * st["loop_wave_iters"], 1),
             "bvh_loop": st["trav_lane_steps"] / max(64 * st["trav_wave_steps"], 1)}
     if world > 1:
@@ -355,7 +406,8 @@ def main():
     if rank == 0:
         # dominant kernel = k_render_ps; algorithmic bytes of rank 0's launch
         compact = compact_nodes(info)
-        kernel = dominant_kernel(compact, int(info.get("ps_waves", 5)), info["n_tris"] > 0)
+        kernel = dominant_kernel(compact, int(info.get("ps_waves", 5)), info["n_tris"] > 0,
+                                 bool(info.get("ps_park", 0)))
         node_b = CNODE_BYTES if compact else NODE_BYTES
         bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
@@ -364,7 +416,7 @@ def main():
         # only: the entry must carry the running library's build id (a hash of the kernel
         # sources and flags, wgt_build_id), else they are null with the reason
         build_id = w.build_id()
-        traffic, l2, tj_id = None, None, None
+        traffic, l2, tj_id, sq, write_b = None, None, None, None, None
         traffic_note = "no profile entry for this workload"
         try:
             with open(args.traffic_json) as f:
@@ -380,6 +432,7 @@ def main():
             if tj and tj_id == build_id and tj.get("n_gpus", 1) == 1 and world == 1 and tj.get("kernel") == kernel:
                 traffic_note = f"PMC passes of build {build_id} ({tj.get('source')})"
                 traffic = tj.get("hbm_bytes_per_launch")
+                sq, write_b = tj.get("sq"), tj.get("write_bytes_per_launch")
                 req = tj.get("tcc_requests_per_launch")
                 with open(L2_CALIB_JSON) as f:
                     bpr = json.load(f)["bytes_per_request"]
@@ -397,6 +450,7 @@ def main():
             live, note = live_pmc(args, kernel)
             if live is not None:
                 traffic, tj_id, traffic_note, traffic_source = live["hbm_bytes_per_launch"], build_id, note, "live"
+                sq, write_b = live["sq"], live["write_bytes_per_launch"]
                 req = live["tcc_requests_per_launch"]
                 with open(L2_CALIB_JSON) as f:
                     bpr = json.load(f)["bytes_per_request"]
@@ -408,6 +462,7 @@ def main():
                           "calibration": os.path.relpath(L2_CALIB_JSON, ROOT)}
             else:
                 traffic_note = f"{note}; {traffic_note}"
+        hbm_frac = round(traffic / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if traffic and kern_ms > 0 else None
         nodes = [int(x["node_visits"]) for x in sts]
         tris = [int(x["tri_tests"]) for x in sts]
         n_tris = info["n_tris"]
@@ -443,12 +498,19 @@ def main():
                            "algorithmic_bytes": int(survey_bytes), "loaded_bytes": int(bytes_launch),
                            "kernel": kernel, "bvh_nodes": "compact 64 B + 16 B refs" if compact else "128 B"},
             # achieved = SURVEY 8(d)'s algorithmic bytes (32 B per node visit, 48 B per triangle test, 32 B
-            # per traced ray: independent of the node encoding) / the launch time
-            "roofline": {"bound": "hbm", "achieved": round(survey_bytes / (kern_ms * 1e-3) / 1e9, 2) if kern_ms > 0
+            # per traced ray: independent of the node encoding) / the launch time.  The roofline priced is
+            # HBM's; `bound` is what the measurements show bounds the kernel (limiter())
+            "roofline": {"bound": limiter(hbm_frac, sq), "achieved": round(survey_bytes / (kern_ms * 1e-3) / 1e9, 2) if kern_ms > 0
                          else 0.0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(survey_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if kern_ms > 0
                          else 0.0, "traffic": traffic, "traffic_build_id": tj_id if traffic is not None else None,
                          "traffic_source": traffic_source, "traffic_note": traffic_note,
+                         # measured HBM traffic / launch time / peak: the DRAM side of the roofline
+                         "hbm_frac": hbm_frac, "write_bytes_per_launch": write_b,
+                         # SQ pass: VALU pipes busy, and wave cycles issuing / in s_waitcnt / ready
+                         # but not issued (sq_fields)
+                         "valu_busy": sq["valu_busy"] if sq else None,
+                         "wave_split": sq["wave_split"] if sq else None,
                          "bytes_per_unit": {"node": SURVEY_NODE_BYTES, "tri": SURVEY_TRI_BYTES,
                                             "shade_per_ray": SHADE_BYTES},
                          # the bytes this implementation's encodings load per launch (80-B compact or 112-B
@@ -466,6 +528,16 @@ def main():
             "cpu_baseline": base,
             "build_id": build_id,
         }
+        if world > 1:
+            # where a multi-GPU step's time goes: each rank's launch time and its gather (which
+            # waits for the slowest rank's tiles), per step
+            line["per_rank"] = {"kernel_ms": [round(float(x), 3) for x in allv[:, 6]],
+                                "gather_ms": [round(float(x), 3) for x in allv[:, 7]],
+                                "isolated_launch_ms": [round(float(x), 3) for x in allv[:, 8]],
+                                "kernel_ms_min_max": [round(float(allv[:, 6].min()), 3),
+                                                      round(float(allv[:, 6].max()), 3)],
+                                "gather_ms_min_max": [round(float(allv[:, 7].min()), 3),
+                                                      round(float(allv[:, 7].max()), 3)]}
         if check is not None:
             line["check_frames_bit_exact"] = check
             line["check"] = {"frames": len(frames), "world_size": world,

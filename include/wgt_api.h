@@ -113,14 +113,17 @@ typedef struct {
   uint64_t loop_wave_iters, loop_lane_iters, trav_wave_steps, trav_lane_steps;
   /* phase-split kernel: wave cycles (s_memtime) in the service / traversal phase */
   uint64_t cyc_service, cyc_trav;
-  float kernel_ms;       /* hipEvent time of the (uninstrumented) render launches of the frame */
-  float trace_ms;        /* ... of which BVH-traversal kernel launches (wavefront) */
-  float shade_ms;        /* ... of which shading kernel launches (wavefront) */
-  uint32_t iterations;   /* wavefront bounce iterations (1 for a megakernel launch) */
+  float kernel_ms;       /* hipEvent time of the (uninstrumented) render launch of the frame */
+  float trace_ms;        /* = kernel_ms (one launch traces and shades; kept for the layout) */
+  float shade_ms;        /* 0 (kept for the layout) */
+  uint32_t iterations;   /* launches per frame: 1 */
   /* phase-split kernel: wave cycles of the service phase by region: pixel refill +
    * writes, finalise (quad rebuild, triangle merge, spheres), shading, camera ray +
    * NaN handling, quad scan, root-node test */
   uint64_t cyc_refill, cyc_finalise, cyc_shade, cyc_camera, cyc_quads, cyc_root;
+  /* persistent kernel with parked traversal state: LDS stack overflows moved to the
+   * lane's global stack, and refills from it */
+  uint64_t stack_spills, stack_refills;
 } wgt_stats;
 
 typedef struct {
@@ -134,8 +137,11 @@ typedef struct {
   uint32_t bvh_compact;   /* 1: the tree exceeds one XCD's L2 as 128-B nodes, so the persistent
                            * kernel reads its compact form (64-B nodes + 16-B refs) by default */
   float bvh_compact_step; /* scene-wide decode step of the compact nodes (wgt_geom.h) */
-  uint32_t ps_waves;      /* waves per SIMD of the persistent kernel: 6 when the tree collapses
-                           * under the 25-entry stack bound at <= 3% more nodes, else 5 */
+  uint32_t ps_waves;      /* waves per SIMD of the persistent kernel: 6 with 3-byte stack entries
+                           * when every ref of the tree fits 24 bits, else 5 */
+  uint32_t ps_park;       /* 1: the persistent kernel parks its traversal state in LDS during
+                           * service passes */
+  uint32_t ps_stack;      /* stack entries per lane it keeps in LDS (the rest: a global stack) */
 } wgt_scene_info;
 
 typedef struct wgt_ctx wgt_ctx;
@@ -201,9 +207,7 @@ int wgt_render_frames(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uin
  * on the device only for the previous launch that used the same workspace: two
  * consecutive calls on different streams may run concurrently (the next frame's
  * waves fill the CUs the previous frame's end-of-launch drain leaves idle), so the
- * caller gives such calls distinct output buffers.  The one exception is the
- * wavefront kernel family (WGT_KERNEL=0, off by default), whose host loop polls a
- * device completion counter and returns when the frame is done.  wgt_upload_scene
+ * caller gives such calls distinct output buffers.  wgt_upload_scene
  * and wgt_destroy wait for every launch of the context before freeing what it
  * reads. */
 int wgt_render_tiles_async(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uint32_t H,

@@ -44,7 +44,7 @@ def test_struct_sizes_match_reference_layouts(wgt):
     assert _lib.SPHERE_DTYPE.itemsize == 32    # scene.h:47 sphere_stride_
     assert _lib.TRI_DTYPE.itemsize == 80       # scene.h:45 tri_stride_
     assert _lib.CAMERA_DTYPE.itemsize == 48    # camera.h:19-31
-    assert ctypes.sizeof(_lib.WgtStats) == 168
+    assert ctypes.sizeof(_lib.WgtStats) == 184  # + stack_spills, stack_refills (round 4)
 
 
 def test_version(wgt):

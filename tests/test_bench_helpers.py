@@ -1,0 +1,43 @@
+"""CPU checks of bench.py's measurement arithmetic (no GPU): the SQ-pass figures (VALU-busy
+fraction, wave-cycle split) and the limiter that sets roofline.bound from them."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+
+
+def test_sq_fields_round3_profile():
+    """The round-3 sponza PMC pass (profiles/r03_r03r_summary.md, one launch): 6,144 waves,
+    1,051.2e9 wave quad-cycles, 227.4e9 VALU instructions -> the 0.34 / 0.39 / 0.27 split and
+    VALU pipes busy ~0.65 of the launch."""
+    agg = {"SQ_WAVES": 6144.0, "SQ_WAVE_CYCLES": 1051221112734.0, "SQ_WAIT_ANY": 407607722278.0,
+           "SQ_WAIT_INST_ANY": 285739843156.0, "SQ_ACTIVE_INST_ANY": 357873547300.0,
+           "SQ_INSTS_VALU": 227429489776.0}
+    sq = bench.sq_fields(agg, 1)
+    ws = sq["wave_split"]
+    assert (ws["issuing"], ws["waiting"], ws["issue_stalled"]) == (0.3404, 0.3877, 0.2718)
+    launch_cycles = 4 * 1051221112734.0 / 6144
+    assert abs(sq["valu_busy"] - 227429489776.0 * 2 / (1024 * launch_cycles)) < 1e-4
+    assert 0.6 < sq["valu_busy"] < 0.7
+    # two launches aggregated: the same per-launch figures
+    sq2 = bench.sq_fields({k: 2 * v for k, v in agg.items()}, 2)
+    assert sq2["valu_busy"] == sq["valu_busy"] and sq2["wave_split"] == ws
+    assert bench.sq_fields({}, 1) is None
+
+
+def test_limiter():
+    assert bench.limiter(0.8, None) == "hbm"
+    assert bench.limiter(0.375, {"valu_busy": 0.75}) == "valu"
+    assert bench.limiter(0.375, {"valu_busy": 0.65}) == "latency"
+    assert bench.limiter(None, None) == "unmeasured"
+
+
+def test_dominant_kernel_names():
+    """The rocprof kernel names bench.py matches its PMC rows against (k_render_ps's template
+    arguments <STATS, COST, CN, W, TRIS, PK>)."""
+    assert bench.dominant_kernel(True, 6) == "wgt::k_render_ps<false, false, true, 6, true, true>"
+    assert bench.dominant_kernel(False, 5, park=False) == "wgt::k_render_ps<false, false, false, 5, true, false>"
+    assert bench.dominant_kernel(True, 6, tris=False) == "wgt::k_render_ps<false, false, false, 8, false, false>"

@@ -301,14 +301,12 @@ def test_sponza_1080p_256spp_subsample_compact(ctx, wgt, oracle):
         assert np.array_equal(g["hit"], r["hit"])
 
 
-@pytest.mark.parametrize("kernel", ["0", "1", "2"])
+@pytest.mark.parametrize("kernel", ["1", "2"])
 def test_kernel_families_agree_with_oracle(ctx, wgt, oracle, bunny, kernel, monkeypatch):
-    """wavefront (0), simple megakernel (1) and phase-split megakernel (2) are all
+    """The simple megakernel (1) and the persistent phase-split one (2) are both
     bit-exact against the oracle (the tuning knobs change speed only)."""
     (L, Q, S, T), osc = bunny
     monkeypatch.setenv("WGT_KERNEL", kernel)
-    monkeypatch.setenv("WGT_WF_RAYS", "2")
-    monkeypatch.setenv("WGT_WF_CHUNK", "256")
     ctx.upload_scene(L, Q, S, T)
     g = ctx.render_tile(wgt.camera_param(16 / 9, 4, 21), 72, 40, stats=True)
     r = osc.render(oracle.camera_param(16 / 9, 4, 21), 72, 40)
@@ -327,17 +325,21 @@ _SCHED_REF = {}
                                  {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
                                  {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}, {"WGT_NARROW": "1"},
                                  {"WGT_STACK_LIMIT": "20"},
-                                 # the workgroup ray pool (wgt_pool.hip, opt-in): rays move between lanes
-                                 {"WGT_POOL": "6"}, {"WGT_POOL": "5"}, {"WGT_POOL": "6", "WGT_CNODE": "1"},
-                                 {"WGT_POOL": "5", "WGT_PS_TO_TRAV": "48", "WGT_PS_TO_SERVICE": "46"}])
+                                 # parked traversal state with the smallest LDS stack (every node
+                                 # step near the top spills to the global stack), per node form and
+                                 # wave budget; and the whole stack in LDS (WGT_PARK=0)
+                                 {"WGT_PS_CAP": "5"}, {"WGT_PS_CAP": "5", "WGT_CNODE": "1"},
+                                 {"WGT_PS_CAP": "6", "WGT_PS_WAVES": "5"}, {"WGT_PS_CAP": "9", "WGT_PQ_LPT": "0"},
+                                 {"WGT_PARK": "0"}, {"WGT_PARK": "0", "WGT_CNODE": "1"},
+                                 ])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the
     cost pre-pass (1 or 4 spp) or block order; refill threshold; phase thresholds and
     their sparse-wave scaling; the node form: compact nodes forced on the bunny; the
     wave budget: 6 waves per SIMD with 3-byte stack entries or, with WGT_PS_WAVES=5, 5
     with 4-byte ones; the narrow 25-entry tree, WGT_NARROW=1; a 20-entry bound, which moves
-    the 3-byte stack's byte array; the workgroup ray pool, WGT_POOL, whose rays are
-    traversed by lanes of other waves)
+    the 3-byte stack's byte array; the parked traversal state with small LDS stacks,
+    WGT_PS_CAP, and the whole stack in LDS, WGT_PARK=0)
     change which lane renders which pixel and when, never a bit of the result.  100x60
     leaves ragged 8x8 blocks at the frame edge.  The test runs after the kernel-family
     tests on the same context, the sequence that exposed a workspace-reuse bug (each
@@ -354,6 +356,29 @@ def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     assert_radiance(g["f32"], r["f32"])
     assert np.array_equal(g["hit"], r["hit"])
     check_counters(g["stats"], r["counters"], oracle)
+
+
+@pytest.mark.parametrize("cap,cnode", [("5", "2"), ("5", "1"), ("7", "2")])
+def test_stack_overflow_spill_and_refill(ctx, wgt, oracle, bunny, cap, cnode, monkeypatch):
+    """The parked kernel's LDS stack bounded at 5 (or 7) entries (WGT_PS_CAP, the builder's
+    bound is 31): node steps that leave fewer than 4 free entries park the lane, whose
+    service pass moves the bottom of its stack to the global stack, and a lane whose LDS
+    part runs empty refills from it (park_fix).  Both paths must
+    run (the counters) and the frame stay bit-exact against the oracle."""
+    (L, Q, S, T), osc = bunny
+    monkeypatch.setenv("WGT_PS_CAP", cap)
+    monkeypatch.setenv("WGT_CNODE", cnode)
+    ctx.upload_scene(L, Q, S, T)
+    info = ctx.scene_info()
+    assert info["ps_park"] == 1 and info["ps_stack"] == int(cap) < info["bvh_stack"]
+    g = ctx.render_tile(wgt.camera_param(5 / 3, 9, 3), 100, 60, stats=True)
+    if "r" not in _SCHED_REF:
+        _SCHED_REF["r"] = osc.render(oracle.camera_param(5 / 3, 9, 3), 100, 60)
+    r = _SCHED_REF["r"]
+    assert_radiance(g["f32"], r["f32"])
+    assert np.array_equal(g["hit"], r["hit"])
+    check_counters(g["stats"], r["counters"], oracle)
+    assert g["stats"]["stack_spills"] > 0 and g["stats"]["stack_refills"] > 0
 
 
 def test_mesh_tiles_reassemble_full_frame(ctx, wgt, bunny):

@@ -271,6 +271,12 @@ def test_bench_two_ranks_self_checks(tmp_path):
     line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["check_frames_bit_exact"] is True
     assert line["check"]["world_size"] == 2 and line["check"]["frames"] == 2
+    # where the step's time goes at N > 1: each rank's launch and gather time
+    pr = line["per_rank"]
+    assert len(pr["kernel_ms"]) == 2 and len(pr["gather_ms"]) == 2 and len(pr["isolated_launch_ms"]) == 2
+    assert all(x > 0 for x in pr["kernel_ms"]) and all(x >= 0 for x in pr["gather_ms"])
+    assert pr["kernel_ms_min_max"] == [min(pr["kernel_ms"]), max(pr["kernel_ms"])]
+    assert pr["gather_ms_min_max"] == [min(pr["gather_ms"]), max(pr["gather_ms"])]
 
 
 def test_bench_line_contract(tmp_path):
@@ -294,8 +300,18 @@ def test_bench_line_contract(tmp_path):
     assert line["unit"] == "Mrays/s" and line["higher_is_better"] is True and line["dtype"] == "f32"
     assert line["config"]["workload"] == "bunny-96x64-4spp"
     rf = line["roofline"]
-    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["peak"] > 0
+    assert rf["unit"] == "GB/s" and rf["peak"] > 0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # what bounds the kernel, from the run's own measurements (bench.limiter): the measured HBM
+    # traffic's share of the peak, the VALU-busy fraction and the wave-cycle split
+    assert abs(rf["hbm_frac"] - rf["traffic"] / (line["kernel_ms"] * 1e-3) / 1e9 / rf["peak"]) < 1e-3
+    assert 0.0 < rf["valu_busy"] < 1.5 and rf["write_bytes_per_launch"] >= 0
+    ws = rf["wave_split"]
+    assert abs(ws["issuing"] + ws["waiting"] + ws["issue_stalled"] - 1.0) < 0.05
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert rf["bound"] == bench.limiter(rf["hbm_frac"], {"valu_busy": rf["valu_busy"]})
     # the per-launch time of pipelined frames cannot undercount the wall time per step at small K
     # (the first-to-last completion interval did: two frames in flight complete in pairs)
     assert line["kernel_ms"] <= line["ms_per_step"] * 1.001

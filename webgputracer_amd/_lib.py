@@ -40,7 +40,8 @@ class WgtStats(ctypes.Structure):
                 ("trace_ms", ctypes.c_float), ("shade_ms", ctypes.c_float), ("iterations", ctypes.c_uint32),
                 ("cyc_refill", ctypes.c_uint64), ("cyc_finalise", ctypes.c_uint64),
                 ("cyc_shade", ctypes.c_uint64), ("cyc_camera", ctypes.c_uint64), ("cyc_quads", ctypes.c_uint64),
-                ("cyc_root", ctypes.c_uint64)]
+                ("cyc_root", ctypes.c_uint64), ("stack_spills", ctypes.c_uint64),
+                ("stack_refills", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -52,7 +53,8 @@ class WgtSceneInfo(ctypes.Structure):
                 ("bvh_max_depth", ctypes.c_uint32), ("bvh_max_leaf", ctypes.c_uint32),
                 ("device_bytes", ctypes.c_uint64), ("sah_cost", ctypes.c_double), ("bvh_width", ctypes.c_uint32),
                 ("bvh_stack", ctypes.c_uint32), ("bvh2_nodes", ctypes.c_uint32), ("bvh2_depth", ctypes.c_uint32),
-                ("bvh_compact", ctypes.c_uint32), ("bvh_compact_step", ctypes.c_float), ("ps_waves", ctypes.c_uint32)]
+                ("bvh_compact", ctypes.c_uint32), ("bvh_compact_step", ctypes.c_float), ("ps_waves", ctypes.c_uint32),
+                ("ps_park", ctypes.c_uint32), ("ps_stack", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

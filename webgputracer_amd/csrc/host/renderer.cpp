@@ -7,6 +7,7 @@
 #include "../../../include/wgt/renderer.h"
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <iomanip>
 #include <iostream>
@@ -110,15 +111,22 @@ bool Renderer::OnRenderBatch(uint32_t first, uint32_t n) {
     std::cerr << "[WebGPUTracer] render failed: " << wgt_last_error(ctx_) << std::endl;
     return false;
   }
-  if (cfg_.write_png) {  // the batch's PNGs are encoded concurrently, one thread per frame
+  if (cfg_.write_png) {
+    // the batch's PNGs are encoded concurrently by at most hardware_concurrency (and 16)
+    // writers, each taking the next frame of the batch
     std::vector<int> rc(n, WGT_OK);
+    std::atomic<uint32_t> next{0};
+    const uint32_t hw = std::max(1u, std::thread::hardware_concurrency());
+    const uint32_t n_writers = std::min({n, hw, 16u});
     std::vector<std::thread> writers;
-    for (uint32_t j = 0; j < n; ++j) {
-      writers.emplace_back([&, j] {
-        std::ostringstream sout;
-        sout << std::setw(3) << std::setfill('0') << first + j;
-        const std::string output_file = cfg_.out_dir + "/" + sout.str() + ".png";
-        rc[j] = wgt_write_png(output_file.c_str(), images.data() + frame_bytes * j, cfg_.width, cfg_.height);
+    for (uint32_t k = 0; k < n_writers; ++k) {
+      writers.emplace_back([&] {
+        for (uint32_t j = next++; j < n; j = next++) {
+          std::ostringstream sout;
+          sout << std::setw(3) << std::setfill('0') << first + j;
+          const std::string output_file = cfg_.out_dir + "/" + sout.str() + ".png";
+          rc[j] = wgt_write_png(output_file.c_str(), images.data() + frame_bytes * j, cfg_.width, cfg_.height);
+        }
       });
     }
     for (auto& t : writers) t.join();

@@ -1,5 +1,4 @@
-// wgt_device.h — device building blocks of the path tracer shared by the
-// megakernels (wgt_kernels.hip) and the wavefront kernels (wgt_wavefront.hip).
+// wgt_device.h — device building blocks of the path tracer kernels (wgt_kernels.hip).
 // Each function restates one piece of resources/shader/path_tracer.wgsl (cited
 // per function); both kernel families therefore compute bit-identical results.
 #pragma once
@@ -138,6 +137,7 @@ __device__ __forceinline__ void nan_hit(const DevScene& sc, f3 o, f3 d, Hit& h) 
 
 struct TravStats {
   uint32_t nodes, tris, wave_steps, lane_steps;
+  uint32_t spills, refills;  // parked k_render_ps: global-stack moves (park_fix)
 };
 
 // Counts one per wave (first active lane) and one per active lane.
@@ -393,8 +393,7 @@ constexpr int kNoRef = 0x7fffffff;
 // of a tree with fewer than 2^16 nodes and 2^20 triangles (byte offsets < 2^23,
 // leaf refs >= -2^23; DevScene::ps_waves) and lets LDS hold the full 31-entry
 // bound of 24 waves per CU: 6 waves per SIMD without a narrower tree.
-// S: the stride in entries (kBlock for one wave per block; the ray-pool kernel's
-// workgroup-wide columns use its block size, wgt_pool.hip).
+// S: the stride in entries (kBlock: one wave per block).
 template <int S = kBlock>
 struct Stack32S {
   int* __restrict__ p;
@@ -413,6 +412,44 @@ struct Stack24S {
 };
 using Stack32 = Stack32S<>;
 using Stack24 = Stack24S<>;
+
+// Parked traversal state of k_render_ps (DevScene::ps_park): the
+// lane's Trav lives in LDS words (stride kBlock, conflict-free) while its wave runs a
+// service pass, so the service code does not hold the traversing lanes' 11 registers and
+// needs no scratch.  Word 9 holds the LDS stack top in its low half and the depth of the
+// lane's global stack (entries moved out of LDS, DevFrame::ps_spill) in its high half:
+// the traversal phase reads and writes only the low half.  The open leaf is one word:
+// the record offset (a multiple of kTriRecordBytes = 64) plus the records left (<= 8).
+struct Park {
+  uint32_t* __restrict__ p;
+  __device__ __forceinline__ uint32_t ld(int j) const { return p[j * kBlock]; }
+  __device__ __forceinline__ void st(int j, uint32_t v) const { p[j * kBlock] = v; }
+  __device__ __forceinline__ uint32_t sp() const { return ((const uint16_t*)(p + 9 * kBlock))[0]; }
+  __device__ __forceinline__ void set_sp(uint32_t v) const { ((uint16_t*)(p + 9 * kBlock))[0] = (uint16_t)v; }
+};
+static_assert(kTriRecordBytes == 64, "the parked open leaf packs its count into the offset's low 6 bits");
+__device__ __forceinline__ uint32_t park_leaf(const Trav& t) { return t.lf | ((t.le - t.lf) / kTriRecordBytes); }
+__device__ __forceinline__ void unpark_leaf(uint32_t w, Trav& t) {
+  t.lf = w & ~63u;
+  t.le = t.lf + (w & 63u) * kTriRecordBytes;
+}
+// the whole state; the global depth (word 9's high half) is left as it is
+__device__ __forceinline__ void park_put(const Park& P, const Trav& t) {
+  P.st(0, __float_as_uint(t.inv.x)); P.st(1, __float_as_uint(t.inv.y)); P.st(2, __float_as_uint(t.inv.z));
+  P.st(3, __float_as_uint(t.ot.x)); P.st(4, __float_as_uint(t.ot.y)); P.st(5, __float_as_uint(t.ot.z));
+  P.st(6, __float_as_uint(t.bt)); P.st(7, t.bi); P.st(8, (uint32_t)t.ref);
+  P.set_sp((uint32_t)t.sp);
+  P.st(10, park_leaf(t));
+}
+__device__ __forceinline__ void park_get(const Park& P, Trav& t) {
+  t.inv = f3{__uint_as_float(P.ld(0)), __uint_as_float(P.ld(1)), __uint_as_float(P.ld(2))};
+  t.ot = f3{__uint_as_float(P.ld(3)), __uint_as_float(P.ld(4)), __uint_as_float(P.ld(5))};
+  t.bt = __uint_as_float(P.ld(6));
+  t.bi = P.ld(7);
+  t.ref = (int)P.ld(8);
+  t.sp = (int)P.sp();
+  unpark_leaf(P.ld(10), t);
+}
 
 // Place `cand` (a child ref, or kNoRef = take the next stack entry).
 template <class STK>
@@ -442,6 +479,43 @@ __device__ __forceinline__ void trav_resolve(const DevScene& sc, Trav& t, int ca
 }
 
 __device__ __forceinline__ bool trav_done(const Trav& t) { return t.ref == kNoRef && t.lf >= t.le && t.sp == 0; }
+
+// Parked k_render_ps: a lane leaves its traversal phase when a node step leaves fewer than
+// 4 free LDS entries above its stack top (the next step's 3 pushes and a parked leaf), or
+// when its LDS stack runs empty with entries still on its global stack.  Its service pass
+// then moves stack entries between LDS and the lane's global stack (gs, stride `stride`)
+// and the traversal resumes: the stack keeps its order, split over the two, so the
+// traversal visits what the whole-LDS stack would (it only stops early when the LDS part
+// runs empty, which any order of the exact min (t, index) search allows).
+// Returns 1 for a spill, 2 for a refill.
+template <class STK>
+__device__ __forceinline__ uint32_t park_fix(const DevScene& sc, const Park& P, const STK& lds, uint32_t cap,
+                                             int* __restrict__ gs, uint32_t stride) {
+  const uint32_t w9 = P.ld(9);
+  const uint32_t sp = w9 & 0xffffu, g = w9 >> 16;
+  if (sp + 4u > cap) {  // overflow: all but the top `keep` entries move to the global stack
+    const uint32_t keep = (cap - 3u) / 2u;  // 1 <= keep <= cap - 4 for cap >= kMinPsCap
+    const uint32_t m = sp - keep;
+    for (uint32_t i = 0; i < m; ++i) gs[(size_t)(g + i) * stride] = lds.ld((int)i);
+    for (uint32_t i = 0; i < keep; ++i) lds.st((int)i, lds.ld((int)(i + m)));
+    P.st(9, keep | (g + m) << 16);
+    return 1u;
+  }
+  // the LDS part ran empty (nothing open, g > 0): the top m global entries come back, then
+  // the pop the traversal stopped at; m - 1 <= cap - 4 leaves room for the next node step
+  const uint32_t half = (cap - 3u) / 2u + 1u;
+  const uint32_t m = g < half ? g : half;
+  for (uint32_t i = 0; i < m; ++i) lds.st((int)i, gs[(size_t)(g - m + i) * stride]);
+  Trav t;
+  t.ref = kNoRef;
+  unpark_leaf(P.ld(10), t);
+  t.sp = (int)m;
+  trav_resolve(sc, t, kNoRef, lds);
+  P.st(8, (uint32_t)t.ref);
+  P.st(10, park_leaf(t));
+  P.st(9, (uint32_t)t.sp | (g - m) << 16);
+  return 2u;
+}
 
 // Visit t.ref: bring the nearest hit child to slot 0 (three compare-exchanges: the
 // pairs, then their minima), push the other three unordered, place the nearest.
@@ -771,6 +845,8 @@ __device__ __forceinline__ void flush_counters(unsigned long long* __restrict__ 
   atomicAdd(&counters[CNT_LOOP_LANE], (unsigned long long)c.ll);
   atomicAdd(&counters[CNT_TRAV_WAVE], (unsigned long long)st.wave_steps);
   atomicAdd(&counters[CNT_TRAV_LANE], (unsigned long long)st.lane_steps);
+  if (st.spills) atomicAdd(&counters[CNT_STACK_SPILLS], (unsigned long long)st.spills);
+  if (st.refills) atomicAdd(&counters[CNT_STACK_REFILLS], (unsigned long long)st.refills);
 }
 
 

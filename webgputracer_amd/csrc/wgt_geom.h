@@ -69,8 +69,8 @@ WGT_HD f3 slab_offset(f3 o, f3 inv) { return f3{-(o.x * inv.x), -(o.y * inv.y), 
 // rejected determinant rejects either way (NaN: not rejected, as before).
 // SHORT: 1/det by the short division div_rn (wgt_math.h), exact for 2^-100 <= |det| <=
 // 2^100.  A |det| < 1e-12 is rejected whatever inv_det is, and for render rays |det| <=
-// |e1| |e2| |d| < 2^94 (triangle edge components within 2^30, wgt_runtime.cpp
-// check_scene_limits; primary directions within 2^32, scattered ones unit), so the
+// |e1| |e2| |d| <= 3 sqrt(3) 2^92 < 2^95 (triangle edge components within 2^30, wgt_runtime.cpp
+// check_scene_limits; primary-direction components within 2^32, scattered ones unit), so the
 // result is the IEEE one; caller-supplied rays (k_trace) use IEEE.
 template <bool SHORT = false>
 WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {

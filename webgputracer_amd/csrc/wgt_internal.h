@@ -55,14 +55,34 @@ struct DevScene {
   // k_render_ps waves per SIMD: 6 (3-byte stack entries, Stack24) when every ref of
   // the tree fits 24 bits (kStack24Nodes, kStack24Tris), else 5
   uint32_t ps_waves;
+  // k_render_ps with parked traversal state (ps_park = 1): the
+  // LDS holds ps_cap stack entries per lane (<= stack) plus kParkWords words of the
+  // lane's traversal state; entries beyond ps_cap move to a per-lane global stack
+  // (DevFrame::ps_spill) in the service phase.  ps_park = 0: the whole stack in LDS.
+  uint32_t ps_park, ps_cap;
 };
 constexpr uint32_t kStack24Nodes = 1u << 16;  // 128-B node byte offsets < 2^23
 constexpr uint32_t kStack24Tris = 1u << 20;   // leaf refs ~(first << 3 | count - 1) >= -2^23
+// Parked traversal state per lane (wgt_device.h Park): 1/d (3), slab offsets (3), best t,
+// best index, node ref, stack top | global depth << 16, open leaf (offset | count)
+constexpr uint32_t kParkWords = 11;
+// The smallest LDS stack the parked kernel runs with: a node step needs 4 free entries
+// above the top (3 pushes and a parked leaf) and the top must keep one
+constexpr uint32_t kMinPsCap = 5;
 // Dynamic LDS bytes of a traversal kernel launch (4-byte entries).
 inline size_t stack_lds_bytes(const DevScene& sc) { return (size_t)sc.stack * kBlock * sizeof(int); }
-// ... of a k_render_ps launch: 3-byte entries at 6 waves per SIMD
+// ... of a k_render_ps launch: 3-byte entries at 6 waves per SIMD, ps_cap entries and
+// the parked state when ps_park
 inline size_t ps_stack_lds_bytes(const DevScene& sc) {
-  return sc.ps_waves == 6 ? (size_t)sc.stack * kBlock * 3 : stack_lds_bytes(sc);
+  const size_t entry = sc.ps_waves == 6 ? 3 : sizeof(int);
+  if (sc.ps_park) return (size_t)sc.ps_cap * kBlock * entry + (size_t)kParkWords * kBlock * 4;
+  return (size_t)sc.stack * kBlock * entry;
+}
+// LDS entries the parked kernel can hold at its wave budget: the stack and the parked
+// words of 4 * waves waves per CU within 13 (6 waves) / 16 (5 waves) x 512 B per wave
+inline uint32_t ps_cap_max(uint32_t waves) {
+  const size_t per_wave = waves == 6 ? 13 * 512 : 16 * 512, entry = waves == 6 ? 3 : 4;
+  return (uint32_t)((per_wave - (size_t)kParkWords * kBlock * 4) / (kBlock * entry));
 }
 
 // 1 / spp when spp is a power of two (exact in fp32: end_sample multiplies), else 0
@@ -84,7 +104,7 @@ struct DevFrame {
   // kernel selection and phase-split thresholds (k_render_ps): switch from the
   // service to the traversal phase once >= ps_to_trav lanes traverse, and back
   // once <= ps_to_service lanes still traverse.
-  uint32_t kernel;  // scenes with triangles: 0 = wavefront, 1 = simple, 2 = phase-split (default)
+  uint32_t kernel;  // 2 = the persistent phase-split kernel (default), else the simple one
   uint32_t ps_to_trav, ps_to_service;
   // a wave with fewer live pixels leaves the traversal phase at <= live *
   // ps_svc_frac / 64 traversing lanes (if lower): a sparse wave (the end of a
@@ -96,9 +116,6 @@ struct DevFrame {
   // BVH node form of k_render_ps: 0 = 128-B nodes, 1 = compact nodes, 2 = compact
   // when the 128-B tree exceeds kCompactNodeBytes (default)
   uint32_t cnode;
-  // wavefront: rays a slot may start per shade launch, slots per trace wave,
-  // idle lanes that trigger a refill from the wave's ray list
-  uint32_t wf_rays, wf_chunk, wf_refill;
   // persistent k_render_ps: pixel slots of the launch (64 per 8x8 block), the
   // idle lanes that trigger a refill from the pixel queue, LPT ordering (0 = off,
   // n = order from an n*n-spp cost pre-pass),
@@ -109,38 +126,11 @@ struct DevFrame {
   uint32_t pq_svc_cost;  // pre-pass work units per ray started (a service iteration ~ 7 traversal steps)
   const uint32_t* perm;
   uint32_t* cost;
-  // ray pool (k_render_pool, wgt_pool.hip): 0 = off (k_render_ps), else the pool kernel's
-  // waves per SIMD (6 or 5); ray tickets per wave; idle lanes that trigger an adoption;
-  // whether a wave leaving its traversal parks its own unfinished rays; resident
-  // workgroups on the device (set by the runtime)
-  uint32_t pool, pool_tickets, pool_adopt_min, pool_park, pool_resident;
+  // parked k_render_ps (DevScene::ps_park): the global part of the lanes' stacks, entry e
+  // of the lane (wave w, lane l) at ps_spill[e * ps_spill_stride + w * 64 + l] (launch_render)
+  int* ps_spill;
+  uint32_t ps_spill_stride;
 };
-
-// Wavefront path state, SoA over slots (one slot per pixel of the tile list).
-struct WfState {
-  uint32_t* seed;
-  uint32_t* k;
-  uint32_t* dp;    // depth | phase << 8
-  float* col;      // SoA x[n] y[n] z[n]
-  float* pc;
-  float* ro;
-  float* rd;
-  uint32_t* qprim;
-  float* qt;
-  uint32_t* res_i;  // closest triangle index or kNoHit
-  float* res_t;
-  unsigned long long* ctl;  // [0] slots done
-  uint32_t n;
-};
-size_t wf_state_bytes(uint32_t n);
-hipError_t wf_bind(void* mem, uint32_t n, unsigned long long* ctl, WfState& st);
-hipError_t launch_wf_init(const DevFrame& fr, const wgt_tile* tiles, const WfState& st, uchar4* out8,
-                          float4* out32, uint32_t* outhit, hipStream_t stream);
-hipError_t launch_wf_shade(const DevScene& sc, const DevFrame& fr, const wgt_tile* tiles,
-                           const WfState& st, uchar4* out8, float4* out32, uint32_t* outhit,
-                           unsigned long long* counters, hipStream_t stream);
-hipError_t launch_wf_trace(const DevScene& sc, const DevFrame& fr, const WfState& st,
-                           unsigned long long* counters, hipStream_t stream);
 
 enum {
   CNT_QUERIES = 0,
@@ -162,16 +152,19 @@ enum {
   CNT_CYC_CAMERA,
   CNT_CYC_QUADS,
   CNT_CYC_ROOT,
-  CNT_N = 20
+  CNT_STACK_SPILLS,   // parked k_render_ps: LDS stack overflows moved to the global stack
+  CNT_STACK_REFILLS,  // ... and refills from it
+  CNT_N = 24
 };
 
 // Launchers implemented in wgt_kernels.hip
 // k_render_ps runs persistent: at most `resident` waves (ps_resident_waves),
 // lanes pulling pixel slots from a per-launch queue in LPT order (1-spp cost
 // pre-pass + k_lpt_order), all stream-ordered on `stream`.
-// ws: scheduling workspace of >= render_ws_bytes(fr) bytes, used in stream order
-// (one launch in flight per workspace).
-size_t render_ws_bytes(const DevFrame& fr);
+// ws: scheduling workspace of >= render_ws_bytes(sc, fr, resident) bytes, used in stream
+// order (one launch in flight per workspace): the queues, the LPT costs and order, and the
+// parked kernel's global stacks.
+size_t render_ws_bytes(const DevScene& sc, const DevFrame& fr, uint32_t resident);
 hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
                          uchar4* out8, float4* out32, uint32_t* outhit,
                          unsigned long long* counters, uint32_t resident, void* ws, size_t ws_cap,
@@ -180,12 +173,6 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
 bool use_compact_nodes(const DevScene& sc, const DevFrame& fr);
 // Waves of k_render_ps resident on the whole device for this scene's LDS stack.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves);
-// The ray-pool kernel (wgt_pool.hip): launched by launch_render when fr.pool is set.
-hipError_t launch_pool(const DevScene& sc, const DevFrame& f, bool cn, uint32_t resident_wgs, const wgt_tile* tiles,
-                       uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters, uint32_t* queue,
-                       hipStream_t stream);
-uint32_t pool_tickets_for(int w);  // ray tickets per wave of the pool kernel at w waves per SIMD
-hipError_t pool_resident_wgs(int w, int device, uint32_t& wgs);
 hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d_counts, hipStream_t stream);
 hipError_t launch_trace(const DevScene& sc, const float* d_rays, uint32_t n, uint32_t* prim,
                         float* dist, hipStream_t stream);

@@ -51,7 +51,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
   const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
   f3 ro{}, rd{}, pc{};
   int depth = 0;
-  TravStats st{0u, 0u, 0u, 0u};
+  TravStats st{};
   Counters c{0u, 0u, 0u, 0u, 0u, 1u};  // one pixel per lane
 
   while (!px_done(fr, px)) {
@@ -107,23 +107,30 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
     if (STATS) acc += __builtin_amdgcn_s_memtime() - r0_;     \
   } while (0)
 
-template <bool STATS, bool COST, bool CN, int W, bool TRIS = true>
+// PK (DevScene::ps_park): the lanes' traversal state is parked in
+// LDS words (Park) while the wave runs a service pass, and the LDS holds sc.ps_cap stack
+// entries per lane with the rest on a per-lane global stack (park_fix): the service code
+// then holds no traversal registers, which it used to spill to scratch.
+template <bool STATS, bool COST, bool CN, int W, bool TRIS = true, bool PK = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
             unsigned long long* __restrict__ counters, uint32_t* __restrict__ queue) {
-  extern __shared__ int s_stack[];  // sc.stack entries per lane (ps_stack_lds_bytes)
+  extern __shared__ int s_stack[];  // stack entries per lane (+ parked words), ps_stack_lds_bytes
   // 6 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
   using STK = typename std::conditional<W == 6, Stack24, Stack32>::type;
+  const uint32_t cap = PK ? sc.ps_cap : sc.stack;  // LDS stack entries per lane
   STK lds;
+  Park P;
   if constexpr (W == 6) {
     lds.lo = (uint16_t*)s_stack + threadIdx.x;
-    lds.hi = (int8_t*)((uint16_t*)s_stack + sc.stack * kBlock) + threadIdx.x;
+    lds.hi = (int8_t*)((uint16_t*)s_stack + cap * kBlock) + threadIdx.x;
+    P.p = (uint32_t*)((char*)s_stack + cap * kBlock * 3) + threadIdx.x;
   } else {
     lds.p = s_stack + threadIdx.x;
+    P.p = (uint32_t*)(s_stack + cap * kBlock) + threadIdx.x;
   }
   const uint32_t lane = threadIdx.x;
-  const unsigned long long lt_mask = (1ull << lane) - 1ull;
   const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
   const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
   const uint32_t n_slots = fr.n_slots;
@@ -131,15 +138,23 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   uint32_t po = 0;  // output offset of the lane's pixel
   f3 ro{}, rd{}, pc{};
   int depth = 0;
-  TravStats st{0u, 0u, 0u, 0u};
+  TravStats st{};
   Counters c{0u, 0u, 0u, 0u, 0u, 0u};
   // invariant: trav == !trav_done(t) (a lane leaves the traversal exactly when
   // trav_done turns true), so a lane with a node to visit or a pending leaf is
-  // traversing; a lane starts done
+  // traversing; a lane starts done.  PK: t lives in registers only in the traversal
+  // phase (and while a service pass starts a ray); Park holds it otherwise
   Trav t;
   t.ref = kNoRef;
   t.lf = t.le = 0u;
   t.sp = 0;
+  if (PK) {
+    t.inv = t.ot = f3{0.0f, 0.0f, 0.0f};
+    t.bt = 0.0f;
+    t.bi = kNoHit;
+    park_put(P, t);
+    P.st(9, 0u);
+  }
   uint32_t q_prim = kNoHit;  // quad part of the pending hit, rebuilt at finalisation
   float q_t = kRayMax;
   bool have = false;       // lane holds a pixel
@@ -175,7 +190,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           if ((int)lane == leader) base = atomicAdd(queue, n_idle);
           base = __shfl(base, leader);
           if (!have && !exhausted) {
-            const uint32_t slot = base + (uint32_t)__popcll(idle & lt_mask);
+            // the lane's rank among the idle lanes (mbcnt: the set bits of idle below this lane)
+            const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
             if (slot >= n_slots) {
               exhausted = true;
             } else {
@@ -201,6 +217,22 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       }
       if (need) {
         if (STATS) simt_count(c.lw, c.ll);
+        // PK: a lane whose traversal stopped on its LDS stack (not finished) moves stack
+        // entries to or from its global stack and traverses on
+        bool resume = false;
+        if (PK && TRIS && pending && !nanray) {
+          resume = (int)P.ld(8) != kNoRef || (P.ld(10) & 63u) != 0u || P.ld(9) != 0u;
+          if (resume) {
+            // the lane's global stack: entry e at gs[e * fr.ps_spill_stride]
+            const uint32_t k = park_fix(sc, P, lds, cap, fr.ps_spill + blockIdx.x * kBlock + lane, fr.ps_spill_stride);
+            if (STATS) {
+              st.spills += k == 1u ? 1u : 0u;
+              st.refills += k == 2u ? 1u : 0u;
+            }
+            pending = false;
+            trav = true;
+          }
+        }
         if (pending) {
           // finalise: rebuild the quad hit, merge triangles, scan spheres, shade
           Hit h;
@@ -209,9 +241,12 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             if (STATS) { ++c.q; ++c.nan; }
             nanray = false;
           } else {
+            // the traversal's result (PK: parked)
+            const float bt = PK ? __uint_as_float(P.ld(6)) : t.bt;
+            const uint32_t bi = PK ? P.ld(7) : t.bi;
             // no triangles (TRIS = false): no shading record exists to preload
-            WGT_REGION(cr_fin, float4 pre[2]; if (TRIS) preload_tshade(sc, t, pre[0], pre[1]);
-                       quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, t, h, TRIS ? pre : nullptr));
+            WGT_REGION(cr_fin, float4 pre[2]; if (TRIS) preload_tshade(sc, bi, pre[0], pre[1]);
+                       quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, bt, bi, h, TRIS ? pre : nullptr));
             if (STATS) { ++c.q; ++c.tr; }
           }
           first_hit(px, depth, h.prim, po, outhit);
@@ -226,7 +261,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           pending = false;
         }
         // start the next ray of this pixel
-        for (;;) {
+        for (; !resume;) {
           if (px_done(fr, px)) {
             have = false;
             fin = true;
@@ -259,6 +294,10 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             WGT_REGION(cr_root, root_step<STATS, CN>(sc, t, lds, st));
             if (trav_done(t)) pending = true;
             else trav = true;
+            if (PK) {
+              park_put(P, t);
+              P.st(9, (uint32_t)t.sp);  // a new ray's global stack is empty
+            }
           } else {
             pending = true;  // no triangles: the quad and sphere scans are the whole query
           }
@@ -280,6 +319,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       const uint32_t sparse = (live * fr.ps_svc_frac) >> 6;
       to_service = sparse < to_service ? sparse : to_service;
     }
+    if (PK && TRIS) park_get(P, t);
+    bool parked = false;  // PK: the lane left on its LDS stack bound, its state parked as it was
     for (; TRIS;) {
       // one uniform mode per step: triangle steps once enough lanes hold a
       // pending leaf (weighted by the two steps' costs), else node steps
@@ -293,7 +334,18 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       if (tri_mode) {
         if (can_tri) tri_step<STATS, CN>(sc, ro, rd, t, lds, st);
       } else {
-        if (can_node) node_step<STATS, CN>(sc, t, lds, st);
+        if (can_node) {
+          node_step<STATS, CN>(sc, t, lds, st);
+          // PK: fewer than 4 free LDS entries above the top (only node steps push): the
+          // lane parks its state and leaves as if done; its service pass spills (park_fix)
+          if (PK && (uint32_t)t.sp + 4u > cap) {
+            park_put(P, t);
+            parked = true;
+            t.ref = kNoRef;
+            t.lf = t.le;
+            t.sp = 0;
+          }
+        }
       }
       if (trav && trav_done(t)) {
         trav = false;
@@ -303,6 +355,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       if (ntrav == 0) break;
       if (ntrav <= to_service && __any(!trav && (have || !exhausted))) break;
     }
+    if (PK && TRIS && !parked) park_put(P, t);
     if (STATS) cyc_trav += __builtin_amdgcn_s_memtime() - t_phase;
   }
   if (STATS) {
@@ -330,7 +383,7 @@ k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __res
   const f3 o = f3{rays[i], rays[(size_t)n + i], rays[2 * (size_t)n + i]};
   const f3 d = f3{rays[3 * (size_t)n + i], rays[4 * (size_t)n + i], rays[5 * (size_t)n + i]};
   Hit h;
-  TravStats st{0u, 0u, 0u, 0u};
+  TravStats st{};
   sample_hit<TRIS, false, true>(sc, o, d, s_stack + threadIdx.x, h, st);  // any caller ray: IEEE t
   prim[i] = h.prim;
   dist[i] = h.dist;
@@ -440,6 +493,15 @@ hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d
 // tree would not fit one XCD's 4 MB L2 (sponza stand-in: 8.5 MB -> 4.3 + 1.1 MB);
 // a tree that fits keeps the 128-B nodes, whose step needs fewer VALU.
 // k_render_ps at the scene's waves per SIMD and node form.
+template <bool STATS, bool COST, bool CN, int W>
+void ps_launch_w(const DevScene& sc, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
+                 const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
+                 uint32_t* queue) {
+  if (sc.ps_park)
+    k_render_ps<STATS, COST, CN, W, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+  else
+    k_render_ps<STATS, COST, CN, W, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+}
 template <bool STATS, bool COST>
 void ps_launch(const DevScene& sc, bool cn, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
                const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
@@ -447,11 +509,11 @@ void ps_launch(const DevScene& sc, bool cn, dim3 grid, dim3 block, size_t lds, h
   if (sc.n_tris == 0) {
     k_render_ps<STATS, COST, false, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
   } else if (sc.ps_waves == 6) {
-    if (cn) k_render_ps<STATS, COST, true, 6><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
-    else k_render_ps<STATS, COST, false, 6><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+    if (cn) ps_launch_w<STATS, COST, true, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    else ps_launch_w<STATS, COST, false, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
   } else {
-    if (cn) k_render_ps<STATS, COST, true, 5><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
-    else k_render_ps<STATS, COST, false, 5><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+    if (cn) ps_launch_w<STATS, COST, true, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    else ps_launch_w<STATS, COST, false, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
   }
 }
 
@@ -463,9 +525,16 @@ bool use_compact_nodes(const DevScene& sc, const DevFrame& fr) {
   return fr.cnode == 1 || (fr.cnode == 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes);
 }
 
-size_t render_ws_bytes(const DevFrame& fr) {
+// the parked kernel's global stacks: sc.stack entries per lane of every resident wave
+// (only when the LDS holds fewer, sc.ps_cap < sc.stack)
+size_t ps_spill_bytes(const DevScene& sc, uint32_t resident) {
+  if (!sc.ps_park || sc.n_tris == 0 || sc.ps_cap >= sc.stack) return 0;
+  return (size_t)resident * kBlock * sc.stack * sizeof(int);
+}
+
+size_t render_ws_bytes(const DevScene& sc, const DevFrame& fr, uint32_t resident) {
   const uint64_t bx = (fr.tw + 7u) / 8u, by = (fr.th + 7u) / 8u;
-  return 256 + 8 * bx * by * fr.n_tiles;
+  return ((256 + 8 * bx * by * fr.n_tiles + 255) & ~(uint64_t)255) + ps_spill_bytes(sc, resident);
 }
 
 hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
@@ -482,7 +551,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   if (fr.kernel == 2) {
     const size_t plds = ps_stack_lds_bytes(sc);
     if (blocks * 64ull > 0xffffffffull || resident == 0) return hipErrorInvalidValue;
-    if (!ws || ws_cap < render_ws_bytes(fr)) return hipErrorInvalidValue;
+    if (!ws || ws_cap < render_ws_bytes(sc, fr, resident)) return hipErrorInvalidValue;
     const uint32_t nb = (uint32_t)blocks;
     const dim3 grid(nb < resident ? nb : resident);
     // workspace (the context's, used in stream order): [0] pre-pass queue,
@@ -498,6 +567,11 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
     f.n_slots = nb * 64u;
     f.perm = nullptr;
     f.cost = nullptr;
+    // the global stacks follow the queue, costs and order (render_ws_bytes); the grid has at
+    // most `resident` waves
+    const uint64_t sched = (256 + 8ull * nb + 255) & ~255ull;
+    f.ps_spill = ps_spill_bytes(sc, resident) ? (int*)((char*)ws + sched) : nullptr;
+    f.ps_spill_stride = grid.x * kBlock;
     hipError_t e = hipMemsetAsync(ws, 0, 256 + (lpt ? 4ull * nb : 0), stream);
     if (e == hipSuccess && lpt) {
       DevFrame fc = f;  // the pre-pass: fr.pq_lpt^2 samples per pixel
@@ -512,10 +586,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       f.perm = fc.cost + nb;
       e = hipGetLastError();
     }
-    if (e == hipSuccess && f.pool && tris && sc.ps_waves == 6 && f.pool_tickets && f.pool_resident) {
-      // the ray-pool kernel (wgt_pool.hip); the cost pre-pass above stays k_render_ps
-      e = launch_pool(sc, f, cn, f.pool_resident, d_tiles, out8, out32, outhit, counters, q + 1, stream);
-    } else if (e == hipSuccess) {
+    if (e == hipSuccess) {
       if (counters) ps_launch<true, false>(sc, cn, grid, block, plds, stream, f, d_tiles, out8, out32, outhit, counters, q + 1);
       else ps_launch<false, false>(sc, cn, grid, block, plds, stream, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
       e = hipGetLastError();
@@ -533,19 +604,23 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   return hipGetLastError();
 }
 
+template <int W, bool PK>
+const void* ps_kernel(bool stats, bool cn) {
+  if (stats) return cn ? reinterpret_cast<const void*>(&k_render_ps<true, false, true, W, true, PK>)
+                       : reinterpret_cast<const void*>(&k_render_ps<true, false, false, W, true, PK>);
+  return cn ? reinterpret_cast<const void*>(&k_render_ps<false, false, true, W, true, PK>)
+            : reinterpret_cast<const void*>(&k_render_ps<false, false, false, W, true, PK>);
+}
+
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
-  const bool w6 = sc.ps_waves == 6;
   const void* notris[2] = {reinterpret_cast<const void*>(&k_render_ps<false, false, false, kPsWavesNoTris, false>),
                            reinterpret_cast<const void*>(&k_render_ps<true, false, false, kPsWavesNoTris, false>)};
-  const void* variants[4] = {
-      w6 ? reinterpret_cast<const void*>(&k_render_ps<false, false, false, 6>)
-         : reinterpret_cast<const void*>(&k_render_ps<false, false, false, 5>),
-      w6 ? reinterpret_cast<const void*>(&k_render_ps<true, false, false, 6>)
-         : reinterpret_cast<const void*>(&k_render_ps<true, false, false, 5>),
-      w6 ? reinterpret_cast<const void*>(&k_render_ps<false, false, true, 6>)
-         : reinterpret_cast<const void*>(&k_render_ps<false, false, true, 5>),
-      w6 ? reinterpret_cast<const void*>(&k_render_ps<true, false, true, 6>)
-         : reinterpret_cast<const void*>(&k_render_ps<true, false, true, 5>)};
+  const void* variants[4];
+  for (int i = 0; i < 4; ++i) {
+    const bool stats = i & 1, cn = i >> 1;
+    if (sc.ps_waves == 6) variants[i] = sc.ps_park ? ps_kernel<6, true>(stats, cn) : ps_kernel<6, false>(stats, cn);
+    else variants[i] = sc.ps_park ? ps_kernel<5, true>(stats, cn) : ps_kernel<5, false>(stats, cn);
+  }
   // the largest of the variants' capacities: waves beyond a variant's capacity
   // start as others retire and find the queue drained or nearly so
   int per_cu = 0, cus = 0;

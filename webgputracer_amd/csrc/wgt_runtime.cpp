@@ -46,13 +46,7 @@ struct wgt_ctx {
   wgt_scene_info info{};
   // scratch for the synchronous entry points
   DevBuf tiles, out8, out32, hit, counters, rays, prim, dist;
-  // wavefront path state + completion counter (device) and its pinned mirror
-  DevBuf wf, ctl;
-  unsigned long long* ctl_host = nullptr;
   uint32_t ps_resident = 0;
-  // the ray-pool kernel per waves-per-SIMD budget (index 0: 6, 1: 5): tickets per wave
-  // that keep 6 (5) workgroups per CU, and the resident workgroups at that LDS size
-  uint32_t pool_tickets[2] = {0, 0}, pool_resident[2] = {0, 0};
   // Scheduling workspaces of the persistent kernel (queues, LPT costs and order),
   // used round-robin by its launches.  A launch waits (on the device) only for the
   // previous launch that used the same slot, so consecutive frames issued on two
@@ -69,8 +63,8 @@ struct wgt_ctx {
   // full CU mask, which gives it a hardware queue of its own (two plain streams may
   // share one, and launches on one hardware queue never overlap)
   hipStream_t pipe[kMaxWsSlots] = {};
-  // recorded after every other launch that reads the scene (trace queries, the
-  // wavefront loop); each such launch first waits for the previous one.  The scene
+  // recorded after every other launch that reads the scene (trace queries); each such
+  // launch first waits for the previous one.  The scene
   // and the workspaces are freed (re-upload, destroy, regrow) only after this event
   // and every slot's event have completed
   hipEvent_t use_ev = nullptr;
@@ -160,6 +154,19 @@ uint32_t ps_waves_for(const BvhOut& bvh, uint32_t n_tris) {
   return bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris ? 6u : 5u;
 }
 
+// Parked traversal state of k_render_ps (WGT_PARK=0: the whole
+// stack in LDS): the LDS stack holds what fits beside the parked words at the wave budget,
+// or the whole stack (`stack` entries) when that is smaller; WGT_PS_CAP lowers it, down to
+// kMinPsCap, for tests.
+void ps_park_cap(uint32_t n_tris, uint32_t stack, uint32_t waves, uint32_t& park, uint32_t& cap) {
+  park = n_tris > 0 && env_u32("WGT_PARK", 1) ? 1u : 0u;
+  cap = stack;
+  if (!park) return;
+  uint32_t c = std::min(stack, ps_cap_max(waves));
+  c = std::min(c, std::max(env_u32("WGT_PS_CAP", c), kMinPsCap));
+  cap = std::max(c, kMinPsCap);
+}
+
 DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   DevFrame fr{};
   const float theta = radians_w(cam.fovy);
@@ -197,19 +204,11 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.ps_svc_frac = env_u32("WGT_PS_SVC_FRAC", 16);  // sweep: profiles/sweeps/r01_ps_svc_frac.jsonl
   fr.tri_ratio = env_u32("WGT_TRI_RATIO", 100);
   fr.cnode = env_u32("WGT_CNODE", 2);  // compact nodes once the 128-B tree outgrows an XCD's L2
-  fr.wf_rays = env_u32("WGT_WF_RAYS", 4);
-  fr.wf_chunk = env_u32("WGT_WF_CHUNK", 512);
-  fr.wf_refill = env_u32("WGT_WF_REFILL", 16);
   fr.pq_refill = env_u32("WGT_PQ_REFILL", 0);  // 0 = the default, 2 (launch_render)
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   fr.pq_svc_cost = env_u32("WGT_PQ_SVC_COST", 7);
   fr.pq_lpt_all = env_u32("WGT_PQ_LPT_ALL", 1);  // sweep: all pixels -3% (sponza), -4% (bunny) at 256 spp
-  // the workgroup ray pool (wgt_pool.hip): WGT_POOL = 6 or 5 (waves per SIMD), 0 = off
-  fr.pool = env_u32("WGT_POOL", 0);
-  if (fr.pool != 5 && fr.pool != 6) fr.pool = 0;
-  fr.pool_adopt_min = std::max(env_u32("WGT_POOL_ADOPT", 1), 1u);
-  fr.pool_park = env_u32("WGT_POOL_PARK", 1);
   return fr;
 }
 
@@ -248,7 +247,8 @@ std::string check_scene_limits(const wgt_quad* lq, uint32_t nlq, const wgt_spher
     if (!finite_within(tr[i].v0, 3, kCoordLimit) || !finite_within(tr[i].e1, 3, kCoordLimit) ||
         !finite_within(tr[i].e2, 3, kCoordLimit))
       return "triangle " + std::to_string(i) + ": vertices must be finite and within 2^40";
-    // |det| <= |e1| |e2| |d| < 3 * 2^60 * 2^32 < 2^94: mt_test's short 1/det is exact
+    // |det| <= |e1| |e2| |d| <= (sqrt(3) 2^30)^2 sqrt(3) 2^32 = 3 sqrt(3) 2^92 < 2^95 (edge components
+    // within 2^30, primary-direction components within 2^32): mt_test's short 1/det is exact
     if (!finite_within(tr[i].e1, 3, kEdgeLimit) || !finite_within(tr[i].e2, 3, kEdgeLimit))
       return "triangle " + std::to_string(i) + ": edge components must be within 2^30";
   }
@@ -327,13 +327,14 @@ void fill_stats(const unsigned long long* c, wgt_stats* s) {
   s->cyc_camera = c[CNT_CYC_CAMERA];
   s->cyc_quads = c[CNT_CYC_QUADS];
   s->cyc_root = c[CNT_CYC_ROOT];
+  s->stack_spills = c[CNT_STACK_SPILLS];
+  s->stack_refills = c[CNT_STACK_REFILLS];
 }
 
 
-// Times accumulated over the launches of one frame (profile runs only).
+// Times of one frame's launch (profile runs only).
 struct FrameTiming {
-  float trace_ms = 0.0f, shade_ms = 0.0f, total_ms = 0.0f;
-  uint32_t iterations = 0;
+  float total_ms = 0.0f;
 };
 
 hipEvent_t pool_event(wgt_ctx* ctx, size_t i) {
@@ -345,100 +346,36 @@ hipEvent_t pool_event(wgt_ctx* ctx, size_t i) {
   return ctx->evpool[i];
 }
 
-// Render the tile list: the wavefront loop for scenes with triangles (default),
-// otherwise one megakernel launch.  Blocks until the frame is complete when the
-// wavefront loop runs (it polls a completion counter every few iterations).
+// Render the tile list: one launch of the persistent kernel (or, WGT_KERNEL=1, of the
+// simple one), asynchronous on stream s unless timed.
 int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, uchar4* out8, float4* out32,
                  uint32_t* outhit, unsigned long long* counters, hipStream_t s, FrameTiming* timing) {
-  const bool wavefront = ctx->sc.n_tris > 0 && fr.kernel == 0;
   const uint64_t n64 = (uint64_t)fr.tw * fr.th * fr.n_tiles;
   if (n64 == 0) return WGT_OK;
-  // 32-bit pixel offsets in the kernels (slot_setup, wf slots)
+  // 32-bit pixel offsets in the kernels (slot_setup)
   if (n64 > 0x7fffffffull) return fail(ctx, WGT_E_INVALID, "too many pixels in one launch");
-  if (!wavefront) {
-    hipEvent_t e0 = timing ? pool_event(ctx, 0) : nullptr, e1 = timing ? pool_event(ctx, 1) : nullptr;
-    if (timing && (!e0 || !e1)) return fail(ctx, WGT_E_HIP, "hipEventCreate failed");
-    if (timing) WGT_HIP(ctx, hipEventRecord(e0, s));
-    int rc;
-    // the next workspace slot: a launch on any stream first waits for the previous
-    // launch that used it (WGT_WS_SLOTS = 1 serialises every launch of the context)
-    const uint32_t n_slots = std::min<uint32_t>(std::max<uint32_t>(env_u32("WGT_WS_SLOTS", 2), 1u),
-                                                (uint32_t)wgt_ctx::kMaxWsSlots);
-    wgt_ctx::WsSlot& sl = ctx->slots[ctx->next_slot % n_slots];
-    ctx->next_slot = (ctx->next_slot + 1) % n_slots;
-    const size_t ws_need = render_ws_bytes(fr);
-    if (sl.ws.bytes < ws_need && (rc = use_drain(ctx))) return rc;  // before regrowing
-    if ((rc = ensure(ctx, sl.ws, ws_need))) return rc;
-    if (!sl.ev) WGT_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
-    else WGT_HIP(ctx, hipStreamWaitEvent(s, sl.ev, 0));
-    DevFrame f = fr;
-    if (f.pool) {
-      const int i = f.pool == 6 ? 0 : 1;
-      f.pool_tickets = ctx->pool_tickets[i];
-      f.pool_resident = ctx->pool_resident[i];
-    }
-    WGT_HIP(ctx, launch_render(ctx->sc, f, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
-                               sl.ws.p, sl.ws.bytes, s));
-    WGT_HIP(ctx, hipEventRecord(sl.ev, s));
-    if (timing) {
-      WGT_HIP(ctx, hipEventRecord(e1, s));
-      WGT_HIP(ctx, hipEventSynchronize(e1));
-      WGT_HIP(ctx, hipEventElapsedTime(&timing->total_ms, e0, e1));
-      timing->trace_ms = timing->total_ms;
-      timing->iterations = 1;
-    }
-    return WGT_OK;
-  }
-  const uint32_t n = (uint32_t)n64;
+  hipEvent_t e0 = timing ? pool_event(ctx, 0) : nullptr, e1 = timing ? pool_event(ctx, 1) : nullptr;
+  if (timing && (!e0 || !e1)) return fail(ctx, WGT_E_HIP, "hipEventCreate failed");
+  if (timing) WGT_HIP(ctx, hipEventRecord(e0, s));
   int rc;
-  if ((rc = ensure(ctx, ctx->wf, wf_state_bytes(n)))) return rc;
-  if ((rc = ensure(ctx, ctx->ctl, 256))) return rc;
-  if (!ctx->ctl_host) WGT_HIP(ctx, hipHostMalloc((void**)&ctx->ctl_host, 256, hipHostMallocDefault));
-  WfState st;
-  (void)wf_bind(ctx->wf.p, n, (unsigned long long*)ctx->ctl.p, st);
-  if ((rc = use_begin(ctx, s))) return rc;
-  WGT_HIP(ctx, hipMemsetAsync(ctx->ctl.p, 0, 8, s));
-  size_t ev = 0;
-  auto mark = [&]() -> hipEvent_t {
-    hipEvent_t e = pool_event(ctx, ev++);
-    if (e) (void)hipEventRecord(e, s);
-    return e;
-  };
-  if (timing) mark();
-  WGT_HIP(ctx, launch_wf_init(fr, d_tiles, st, out8, out32, outhit, s));
-  // every slot advances by >= 1 traced ray per iteration; bound the loop anyway
-  const uint64_t nsamp = (uint64_t)fr.sqrt_spp * fr.sqrt_spp;
-  const uint64_t max_iter = nsamp * (uint64_t)(kRayDepth + 1) + 64;
-  const uint32_t check_every = env_u32("WGT_WF_CHECK", 32);
-  uint64_t it = 0;
-  for (;;) {
-    if (timing) mark();
-    WGT_HIP(ctx, launch_wf_shade(ctx->sc, fr, d_tiles, st, out8, out32, outhit, counters, s));
-    if (timing) mark();
-    WGT_HIP(ctx, launch_wf_trace(ctx->sc, fr, st, counters, s));
-    ++it;
-    if (it % check_every == 0 || it >= max_iter) {
-      WGT_HIP(ctx, hipMemcpyAsync(ctx->ctl_host, ctx->ctl.p, 8, hipMemcpyDeviceToHost, s));
-      WGT_HIP(ctx, hipStreamSynchronize(s));
-      if (ctx->ctl_host[0] >= n) break;
-      if (it >= max_iter) return fail(ctx, WGT_E_HIP, "wavefront loop did not converge");
-    }
-  }
-  if ((rc = use_end(ctx, s))) return rc;
+  // the next workspace slot: a launch on any stream first waits for the previous
+  // launch that used it (WGT_WS_SLOTS = 1 serialises every launch of the context)
+  const uint32_t n_slots = std::min<uint32_t>(std::max<uint32_t>(env_u32("WGT_WS_SLOTS", 2), 1u),
+                                              (uint32_t)wgt_ctx::kMaxWsSlots);
+  wgt_ctx::WsSlot& sl = ctx->slots[ctx->next_slot % n_slots];
+  ctx->next_slot = (ctx->next_slot + 1) % n_slots;
+  const size_t ws_need = render_ws_bytes(ctx->sc, fr, ctx->ps_resident);
+  if (sl.ws.bytes < ws_need && (rc = use_drain(ctx))) return rc;  // before regrowing
+  if ((rc = ensure(ctx, sl.ws, ws_need))) return rc;
+  if (!sl.ev) WGT_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
+  else WGT_HIP(ctx, hipStreamWaitEvent(s, sl.ev, 0));
+  WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
+                             sl.ws.p, sl.ws.bytes, s));
+  WGT_HIP(ctx, hipEventRecord(sl.ev, s));
   if (timing) {
-    mark();
-    WGT_HIP(ctx, hipStreamSynchronize(s));
-    // events: [0] init start, then (shade start, trace start) per iteration, [last] end
-    float ms = 0.0f;
-    for (uint64_t i = 0; i < it; ++i) {
-      hipEvent_t a = ctx->evpool[1 + 2 * i], b = ctx->evpool[2 + 2 * i], c = ctx->evpool[3 + 2 * i];
-      WGT_HIP(ctx, hipEventElapsedTime(&ms, a, b));
-      timing->shade_ms += ms;
-      WGT_HIP(ctx, hipEventElapsedTime(&ms, b, c));
-      timing->trace_ms += ms;
-    }
-    WGT_HIP(ctx, hipEventElapsedTime(&timing->total_ms, ctx->evpool[0], ctx->evpool[ev - 1]));
-    timing->iterations = (uint32_t)it;
+    WGT_HIP(ctx, hipEventRecord(e1, s));
+    WGT_HIP(ctx, hipEventSynchronize(e1));
+    WGT_HIP(ctx, hipEventElapsedTime(&timing->total_ms, e0, e1));
   }
   return WGT_OK;
 }
@@ -498,7 +435,6 @@ void wgt_destroy(wgt_ctx* ctx) {
   if (ctx->scene_mem) (void)hipFree(ctx->scene_mem);
   free_buf(ctx->tiles); free_buf(ctx->out8); free_buf(ctx->out32); free_buf(ctx->hit);
   free_buf(ctx->counters); free_buf(ctx->rays); free_buf(ctx->prim); free_buf(ctx->dist);
-  free_buf(ctx->wf); free_buf(ctx->ctl);
   for (auto& sl : ctx->slots) {
     if (sl.ev) (void)hipEventSynchronize(sl.ev);
     free_buf(sl.ws);
@@ -510,7 +446,6 @@ void wgt_destroy(wgt_ctx* ctx) {
     p = nullptr;
   }
   if (ctx->use_ev) (void)hipEventDestroy(ctx->use_ev);
-  if (ctx->ctl_host) (void)hipHostFree(ctx->ctl_host);
   for (hipEvent_t e : ctx->evpool) (void)hipEventDestroy(e);
   if (ctx->ev0) (void)hipEventDestroy(ctx->ev0);
   if (ctx->ev1) (void)hipEventDestroy(ctx->ev1);
@@ -577,6 +512,8 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   info->bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
   info->bvh_compact_step = bvh.cstep;
   info->ps_waves = ps_waves_for(bvh, n_tris);
+  ps_park_cap(n_tris, (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u, info->ps_waves, info->ps_park,
+              info->ps_stack);
   return WGT_OK;
 }
 
@@ -733,18 +670,14 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   // + 1: the speculative traversal parks a second leaf on the stack (wgt_device.h)
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
   sc.ps_waves = ps_waves_for(bvh, n_tris);
+  // parked traversal state (WGT_PARK=0: the whole stack in LDS);
+  // the LDS stack holds what fits beside the parked words at the wave budget, or the whole
+  // stack when that is smaller (WGT_PS_CAP lowers it, down to kMinPsCap, for tests)
+  ps_park_cap(n_tris, sc.stack, sc.ps_waves, sc.ps_park, sc.ps_cap);
   WGT_HIP(ctx, ps_resident_waves(sc, ctx->device, ctx->ps_resident));
-  for (int i = 0; i < 2; ++i) {
-    ctx->pool_tickets[i] = ctx->pool_resident[i] = 0;
-    if (n_tris == 0 || sc.ps_waves != 6) continue;  // the pool records pack 24-bit refs
-    const int w = i == 0 ? 6 : 5;
-    ctx->pool_tickets[i] = pool_tickets_for(w);
-    WGT_HIP(ctx, pool_resident_wgs(w, ctx->device, ctx->pool_resident[i]));
-  }
   if (env_u32("WGT_DEBUG", 0))
-    std::fprintf(stderr, "[wgt] resident: k_render_ps %u waves; pool(6) %u workgroups, %u tickets; "
-                         "pool(5) %u workgroups, %u tickets\n", ctx->ps_resident, ctx->pool_resident[0],
-                 ctx->pool_tickets[0], ctx->pool_resident[1], ctx->pool_tickets[1]);
+    std::fprintf(stderr, "[wgt] resident: k_render_ps %u waves; LDS stack %u of %u entries, parked %u\n",
+                 ctx->ps_resident, sc.ps_cap, sc.stack, sc.ps_park);
 
   wgt_scene_info& in = ctx->info;
   in = wgt_scene_info{};
@@ -765,6 +698,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   in.bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
   in.bvh_compact_step = bvh.cstep;
   in.ps_waves = n_tris ? sc.ps_waves : 0u;
+  in.ps_park = sc.ps_park;
+  in.ps_stack = n_tris ? sc.ps_cap : 0u;
   ctx->has_scene = true;
   return WGT_OK;
 }
@@ -838,9 +773,8 @@ int wgt_render_tiles_profile(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t
     return rc;
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   stats->kernel_ms = timing.total_ms;
-  stats->trace_ms = timing.trace_ms;
-  stats->shade_ms = timing.shade_ms;
-  stats->iterations = timing.iterations;
+  stats->trace_ms = timing.total_ms;
+  stats->iterations = 1;
   return WGT_OK;
 }
 
@@ -874,9 +808,8 @@ int wgt_render_frames(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uin
     rc = wgt_render_tiles_stats(ctx, cam, W, H, W, H, (const wgt_tile*)ctx->tiles.p, n_frames, stats);
     if (rc) return rc;
     stats->kernel_ms = timing.total_ms;
-    stats->trace_ms = timing.trace_ms;
-    stats->shade_ms = timing.shade_ms;
-    stats->iterations = timing.iterations;
+    stats->trace_ms = timing.total_ms;
+    stats->iterations = 1;
   }
   return WGT_OK;
 }
@@ -923,9 +856,8 @@ int wgt_render_tile(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uint3
     rc = wgt_render_tiles_stats(ctx, cam, W, H, tw, th, (const wgt_tile*)ctx->tiles.p, 1, stats);
     if (rc) return rc;
     stats->kernel_ms = timing.total_ms;
-    stats->trace_ms = timing.trace_ms;
-    stats->shade_ms = timing.shade_ms;
-    stats->iterations = timing.iterations;
+    stats->trace_ms = timing.total_ms;
+    stats->iterations = 1;
   }
   return WGT_OK;
 }

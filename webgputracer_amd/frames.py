@@ -136,7 +136,7 @@ def main(argv=None):
     ap.add_argument("--pipeline", type=int, default=2, help="batches in flight (1..4, DESIGN.md §4.2a)")
     ap.add_argument("--out", default=None, help="directory for NNN.png (none: render only)")
     ap.add_argument("--png-threads", type=int, default=0,
-                    help="PNG encoder threads (0: this process's CPU share, capped by OMP_NUM_THREADS)")
+                    help="PNG encoder threads (0: this process's CPU share, capped by OMP_NUM_THREADS and 16)")
     a = ap.parse_args(argv)
     if a.frame[0] < 1 or a.frame[1] < a.frame[0]:
         ap.error("bad frame range")  # the C++ CLI's check (csrc/main.cpp)
@@ -166,7 +166,7 @@ def main(argv=None):
     # PNG encoding (zlib on the host, ~0.5 s per 1080p frame) runs on a thread pool while the GPU
     # renders the next batches (wgt_write_png is a ctypes call: it releases the GIL); at most
     # 4 frames per writer are held
-    workers = max(1, a.png_threads or _cpu_share())
+    workers = max(1, a.png_threads or min(_cpu_share(), 16))
     pool = ThreadPoolExecutor(max_workers=workers) if a.out else None
     pending = collections.deque()
     t0 = time.perf_counter()
