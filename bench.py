@@ -44,7 +44,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # 64-B node + its 16-B ref record; a triangle test all 4 x 16 B of its 64-B record
 # (the padded box with the Moller-Trumbore inputs), a traced
 # ray 32 B of per-triangle shading data
-NODE_BYTES, CNODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 64, 32
+NODE_BYTES, CNODE_BYTES, C64NODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 64, 64, 32
 # SURVEY §8(d)'s format-independent figure: 32 B per BVH node visit, 48 B per triangle
 # test, 32 B of shading record per traced ray (the same at any node encoding)
 SURVEY_NODE_BYTES, SURVEY_TRI_BYTES = 32, 48
@@ -52,20 +52,23 @@ L2_PEAK_GBS = 34500.0  # MI355X_MICROARCH.md §L2: ~34.5 TB/s aggregate over the
 L2_CALIB_JSON = os.path.join(ROOT, "profiles", "l2_calibration.json")
 
 
-def dominant_kernel(compact: bool, waves: int, tris: bool = True, park: bool = True) -> str:
-    """The timed k_render_ps instantiation <STATS, COST, compact nodes, waves per SIMD, triangles,
-    parked traversal state> (a scene without triangles runs the 8-wave instantiation without
-    traversal)."""
+def dominant_kernel(form: int, waves: int, tris: bool = True, park: bool = True) -> str:
+    """The timed k_render_ps instantiation <STATS, COST, node form (0 = 128-B, 1 = 80-B compact,
+    2 = 64-B compact), waves per SIMD, triangles, parked traversal state> (a scene without
+    triangles runs the 8-wave instantiation without traversal)."""
     if not tris:
-        return "wgt::k_render_ps<false, false, false, 8, false, false>"
-    b = lambda x: "true" if x else "false"  # noqa: E731
-    return f"wgt::k_render_ps<false, false, {b(compact)}, {waves}, true, {b(park)}>"
+        return "wgt::k_render_ps<false, false, 0, 8, false, false>"
+    return f"wgt::k_render_ps<false, false, {int(form)}, {waves}, true, {'true' if park else 'false'}>"
 
 
-def compact_nodes(info) -> bool:
-    """The node form k_render_ps reads (WGT_CNODE: 0 = 128-B, 1 = compact, 2 = auto)."""
+def node_form(info) -> int:
+    """The node form k_render_ps reads (wgt_kernels.hip node_form; WGT_CNODE: 0 = 128-B, 1 = 80-B
+    compact, 2 = 80-B compact when the 128-B tree exceeds 4 MB (default), 3 = 64-B compact where the
+    tree fits it (scene_info bvh_c64), else 80-B): 0 = 128-B, 1 = 80-B, 2 = 64-B."""
     mode = os.environ.get("WGT_CNODE", "2") or "2"
-    return mode == "1" or (mode == "2" and bool(info.get("bvh_compact", 0)))
+    if mode == "3":
+        return 2 if info.get("bvh_c64", 0) and info.get("ps_waves") == 6 else 1
+    return 1 if mode == "1" or (mode == "2" and bool(info.get("bvh_compact", 0))) else 0
 
 
 def parse():
@@ -405,10 +408,10 @@ def main():
     base = cpu_baseline(args, scene, rank, world)
     if rank == 0:
         # dominant kernel = k_render_ps; algorithmic bytes of rank 0's launch
-        compact = compact_nodes(info)
-        kernel = dominant_kernel(compact, int(info.get("ps_waves", 5)), info["n_tris"] > 0,
+        form = node_form(info)
+        kernel = dominant_kernel(form, int(info.get("ps_waves", 5)), info["n_tris"] > 0,
                                  bool(info.get("ps_park", 0)))
-        node_b = CNODE_BYTES if compact else NODE_BYTES
+        node_b = (NODE_BYTES, CNODE_BYTES, C64NODE_BYTES)[form]
         bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         survey_bytes = mine[4] * SURVEY_NODE_BYTES + mine[5] * SURVEY_TRI_BYTES + mine[1] * SHADE_BYTES
@@ -496,7 +499,7 @@ def main():
             "simt_utilisation": {k: round(v, 4) for k, v in simt.items()},
             "per_launch": {"traced_rays": int(mine[1]), "node_visits": int(mine[4]), "tri_tests": int(mine[5]),
                            "algorithmic_bytes": int(survey_bytes), "loaded_bytes": int(bytes_launch),
-                           "kernel": kernel, "bvh_nodes": "compact 64 B + 16 B refs" if compact else "128 B"},
+                           "kernel": kernel, "bvh_nodes": ("128 B", "compact 80-B records", "compact 64-B records")[form]},
             # achieved = SURVEY 8(d)'s algorithmic bytes (32 B per node visit, 48 B per triangle test, 32 B
             # per traced ray: independent of the node encoding) / the launch time.  The roofline priced is
             # HBM's; `bound` is what the measurements show bounds the kernel (limiter())

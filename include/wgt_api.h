@@ -142,6 +142,7 @@ typedef struct {
   uint32_t ps_park;       /* 1: the persistent kernel parks its traversal state in LDS during
                            * service passes */
   uint32_t ps_stack;      /* stack entries per lane it keeps in LDS (the rest: a global stack) */
+  uint32_t bvh_c64;       /* 1: the tree also has the 64-B compact form (WGT_CNODE=3) */
 } wgt_scene_info;
 
 typedef struct wgt_ctx wgt_ctx;

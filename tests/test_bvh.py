@@ -231,6 +231,20 @@ def test_wave_budget_and_narrow_tree(monkeypatch):
         info, _, _ = w.bvh_build(w.procedural_mesh(kind))
         assert info["ps_waves"] == 6 and info["bvh_nodes"] < 1 << 16
         assert 25 < info["bvh_stack"] <= 31
+        # the parked kernel keeps 20 of the 32 entries in LDS at 6 waves (3 B each beside 11
+        # parked words: 13 x 512 B per wave), the 64-B compact form fits both trees
+        assert info["ps_park"] == 1 and info["ps_stack"] == 20 and info["bvh_c64"] == 1
+    monkeypatch.setenv("WGT_PS_CAP", "7")
+    info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
+    assert info["ps_stack"] == 7
+    monkeypatch.setenv("WGT_PS_CAP", "2")  # clamped to kMinPsCap
+    info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
+    assert info["ps_stack"] == 5
+    monkeypatch.setenv("WGT_PARK", "0")
+    info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
+    assert info["ps_park"] == 0 and info["ps_stack"] == info["bvh_stack"] + 1
+    monkeypatch.delenv("WGT_PARK")
+    monkeypatch.delenv("WGT_PS_CAP")
     monkeypatch.setenv("WGT_NARROW", "1")
     bunny = w.procedural_mesh("bunny", 20000)
     info = check_tree(bunny)  # the exported (= uploaded) tree passes the full walk

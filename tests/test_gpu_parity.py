@@ -244,10 +244,11 @@ def test_bunny_1080p_256spp_subsample(ctx, wgt, oracle, bunny):
 _SPONZA = {}
 
 
-@pytest.mark.parametrize("cnode", ["2", "0"])
+@pytest.mark.parametrize("cnode", ["2", "0", "3"])
 def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
-    """Sponza stand-in: by default (2) the persistent kernel reads the compact nodes
-    (the 128-B tree exceeds one XCD's L2), 0 forces the 128-B nodes."""
+    """Sponza stand-in: by default (2) the persistent kernel reads the 80-B compact records
+    (the 128-B tree exceeds one XCD's L2), 0 forces the 128-B nodes, 3 the 64-B compact
+    records."""
     monkeypatch.setenv("WGT_CNODE", cnode)
     if not _SPONZA:
         L, Q, S, T = wgt.mesh_scene("sponza")
@@ -263,23 +264,32 @@ def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
     check_counters(g["stats"], r["counters"], oracle)
     info = ctx.scene_info()
     assert info["n_tris"] == len(T) and info["bvh_max_depth"] <= 94
-    assert info["bvh_compact"] == 1
+    assert info["bvh_compact"] == 1 and info["bvh_c64"] == 1
 
 
-@pytest.mark.parametrize("kind,spp", [("sponza", 4), ("bunny", 1)])
-def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp):
+_FULL = {}
+
+
+@pytest.mark.parametrize("kind,spp,cnode", [("sponza", 4, None), ("sponza", 4, "3"), ("bunny", 1, None)])
+def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, cnode, monkeypatch):
     """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
-    oracle (OpenMP), through the default kernel of each scene: sponza on the compact
-    nodes, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries."""
+    oracle (OpenMP), through the default kernel of each scene: sponza on the 80-B compact
+    records, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries and
+    parked traversal state; and sponza on the 64-B compact records (WGT_CNODE=3)."""
+    if cnode is not None:
+        monkeypatch.setenv("WGT_CNODE", cnode)
     L, Q, S, T = wgt.mesh_scene(kind)
     ctx.upload_scene(L, Q, S, T)
     info = ctx.scene_info()
-    if not any(os.environ.get(k) for k in ("WGT_CNODE", "WGT_PS_WAVES", "WGT_STACK_LIMIT")):  # the defaults
+    if not any(os.environ.get(k) for k in ("WGT_CNODE", "WGT_PS_WAVES", "WGT_STACK_LIMIT", "WGT_PARK")):
         assert (info["bvh_compact"], info["ps_waves"]) == ((1, 6) if kind == "sponza" else (0, 6))
-    osc = oracle.OracleScene(L, Q, S, T)
+        assert info["ps_park"] == 1 and info["ps_stack"] == min(20, info["bvh_stack"] + 1)
     g = ctx.render_tile(wgt.camera_param(16 / 9, spp, 3), 1920, 1080, stats=True)
-    r = osc.render(oracle.camera_param(16 / 9, spp, 3), 1920, 1080)
-    osc.close()
+    if kind not in _FULL:
+        osc = oracle.OracleScene(L, Q, S, T)
+        _FULL[kind] = osc.render(oracle.camera_param(16 / 9, spp, 3), 1920, 1080)
+        osc.close()
+    r = _FULL[kind]
     assert_radiance(g["f32"], r["f32"])
     assert np.array_equal(g["hit"], r["hit"])
     check_counters(g["stats"], r["counters"], oracle)
@@ -331,6 +341,9 @@ _SCHED_REF = {}
                                  {"WGT_PS_CAP": "5"}, {"WGT_PS_CAP": "5", "WGT_CNODE": "1"},
                                  {"WGT_PS_CAP": "6", "WGT_PS_WAVES": "5"}, {"WGT_PS_CAP": "9", "WGT_PQ_LPT": "0"},
                                  {"WGT_PARK": "0"}, {"WGT_PARK": "0", "WGT_CNODE": "1"},
+                                 # the 64-B compact records (runtime-selected since round 4)
+                                 {"WGT_CNODE": "3"}, {"WGT_CNODE": "3", "WGT_PS_CAP": "5"},
+                                 {"WGT_CNODE": "3", "WGT_PARK": "0"},
                                  ])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the

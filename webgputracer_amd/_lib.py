@@ -54,7 +54,7 @@ class WgtSceneInfo(ctypes.Structure):
                 ("device_bytes", ctypes.c_uint64), ("sah_cost", ctypes.c_double), ("bvh_width", ctypes.c_uint32),
                 ("bvh_stack", ctypes.c_uint32), ("bvh2_nodes", ctypes.c_uint32), ("bvh2_depth", ctypes.c_uint32),
                 ("bvh_compact", ctypes.c_uint32), ("bvh_compact_step", ctypes.c_float), ("ps_waves", ctypes.c_uint32),
-                ("ps_park", ctypes.c_uint32), ("ps_stack", ctypes.c_uint32)]
+                ("ps_park", ctypes.c_uint32), ("ps_stack", ctypes.c_uint32), ("bvh_c64", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

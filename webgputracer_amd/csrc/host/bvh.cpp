@@ -543,7 +543,7 @@ void CompactNode(const float* n, float s, double G, uint32_t* q) {
   q[3] = 0u;  // reserved
 }
 
-// The 64-B compact form (wgt_geom.h, WGT_CN64): the same codes, relative to an origin on a
+// The 64-B compact form (wgt_geom.h, WGT_CNODE=3): the same codes, relative to an origin on a
 // grid of 512 steps, org/s = 512 K with K a signed byte (stored beside the refs).  q: 16 words,
 // the x, y, z code words (as CompactNode's q[4..15]), then four words whose top bytes hold K
 // for x, y, z and 0 (the upload ORs the 24-bit refs into their low bytes).  false when some

@@ -17,7 +17,7 @@ struct BvhOut {
   std::vector<int32_t> crefs;    // 4 child refs per node (the compact form's ref records)
   float cstep = 1.0f;            // scene-wide decode step of the compact nodes
   float cbound = 0.0f;           // M: the compact codes are exact for ray origins with |o| <= M
-  std::vector<uint32_t> c64;     // 16 words per node: the 64-B compact form without refs (WGT_CN64)
+  std::vector<uint32_t> c64;     // 16 words per node: the 64-B compact form without refs (WGT_CNODE=3)
   float c64step = 1.0f;          // its decode step
   bool c64_ok = false;           // every node's grid origin fits a signed byte
   std::vector<float> tris;    // kTriRecordFloats per triangle, leaf order (wgt_geom.h)

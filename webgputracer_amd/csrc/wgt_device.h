@@ -194,14 +194,21 @@ struct Trav {
 // A triangle was accepted (bi starts at kNoHit, see trav_init).
 __device__ __forceinline__ bool trav_found(const Trav& t) { return t.bi != kNoHit; }
 
-// CN (compact nodes): t.inv holds s/d (s = sc.cstep, a power of two: exact), the
+// The node form CN: 0 = 128-B nodes, 1 = 80-B compact records, 2 = 64-B compact records.
+// A compact form's decode step s (a power of two) and 1/s.
+template <int CN>
+__device__ __forceinline__ float cstep_of(const DevScene& sc) { return CN == 2 ? sc.c64step : sc.cstep; }
+template <int CN>
+__device__ __forceinline__ float rcstep_of(const DevScene& sc) { return CN == 2 ? sc.rc64step : sc.rcstep; }
+
+// CN (compact nodes): t.inv holds s/d (s = the form's step, a power of two: exact), the
 // factor of the fused slab step (cchild_key); the triangle box check multiplies
 // it back by 1/s.
-template <bool CN = false>
+template <int CN = 0>
 __device__ __forceinline__ void trav_init(const DevScene& sc, f3 o, f3 d, bool quad_hit, float qt, Trav& t) {
   t.inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
   t.ot = slab_offset(o, t.inv);
-  if (CN) t.inv = sc.cstep * t.inv;
+  if (CN) t.inv = cstep_of<CN>(sc) * t.inv;
   // a triangle must satisfy t < t_quad to beat a quad hit (ray_dist is monotone in
   // t): with bi = kNoHit the rule "t < bt, or t == bt and index < bi" accepts
   // exactly t <= bt, so bt = the float below t_quad (t_quad > 0).  A box entered
@@ -258,25 +265,28 @@ __device__ __forceinline__ uint32_t cchild_key(const Trav& t, const uint32_t* nw
   const float f = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, t.bt));
   return n <= f ? __float_as_uint(n) : kMissKey;
 }
-template <bool CN>
+template <int CN>
 __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int ref, uint32_t& k0, uint32_t& k1,
                                           uint32_t& k2, uint32_t& k3, int& r0, int& r1, int& r2, int& r3) {
   if (CN) {
-    const float4* __restrict__ n = (const float4*)((const char*)sc.cnodes + (uint32_t)ref);  // ref: byte offset
-#ifdef WGT_CN64
-    const uint4 x = __builtin_bit_cast(uint4, n[0]), y = __builtin_bit_cast(uint4, n[1]),
-                z = __builtin_bit_cast(uint4, n[2]), w = __builtin_bit_cast(uint4, n[3]);
-    const int4 rf = int4{__builtin_amdgcn_sbfe((int)w.x, 0, 24), __builtin_amdgcn_sbfe((int)w.y, 0, 24),
-                         __builtin_amdgcn_sbfe((int)w.z, 0, 24), __builtin_amdgcn_sbfe((int)w.w, 0, 24)};
-    // org/s = 512 K, K the signed top byte: exact
-    const float4 a = float4{__builtin_ldexpf((float)((int)w.x >> 24), 9), __builtin_ldexpf((float)((int)w.y >> 24), 9),
-                            __builtin_ldexpf((float)((int)w.z >> 24), 9), 0.0f};
-#else
-    const int4 rf = __builtin_bit_cast(int4, n[4]);
-    const float4 a = n[0];
-    const uint4 x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]),
-                z = __builtin_bit_cast(uint4, n[3]);
-#endif
+    int4 rf;
+    float4 a;
+    uint4 x, y, z;
+    if constexpr (CN == 2) {  // 64-B record: the codes, then refs and origin packed (wgt_geom.h)
+      const float4* __restrict__ n = (const float4*)((const char*)sc.cnodes64 + (uint32_t)ref);  // byte offset
+      x = __builtin_bit_cast(uint4, n[0]), y = __builtin_bit_cast(uint4, n[1]), z = __builtin_bit_cast(uint4, n[2]);
+      const uint4 w = __builtin_bit_cast(uint4, n[3]);
+      rf = int4{__builtin_amdgcn_sbfe((int)w.x, 0, 24), __builtin_amdgcn_sbfe((int)w.y, 0, 24),
+                __builtin_amdgcn_sbfe((int)w.z, 0, 24), __builtin_amdgcn_sbfe((int)w.w, 0, 24)};
+      // org/s = 512 K, K the signed top byte: exact
+      a = float4{__builtin_ldexpf((float)((int)w.x >> 24), 9), __builtin_ldexpf((float)((int)w.y >> 24), 9),
+                 __builtin_ldexpf((float)((int)w.z >> 24), 9), 0.0f};
+    } else {  // 80-B record: origin, codes, refs
+      const float4* __restrict__ n = (const float4*)((const char*)sc.cnodes + (uint32_t)ref);  // byte offset
+      rf = __builtin_bit_cast(int4, n[4]);
+      a = n[0];
+      x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]), z = __builtin_bit_cast(uint4, n[3]);
+    }
     // c = the slab distance of the node origin org' = (org/s) * s: fma(org/s, s/d, ot)
     const f3 c = f3{__builtin_fmaf(a.x, t.inv.x, t.ot.x), __builtin_fmaf(a.y, t.inv.y, t.ot.y),
                     __builtin_fmaf(a.z, t.inv.z, t.ot.z)};
@@ -525,7 +535,7 @@ __device__ __forceinline__ uint32_t park_fix(const DevScene& sc, const Park& P, 
 // sits: each push advances the top only for a hit.
 // ROOT: the step of a ray that has just started (t.ref = 0 for every lane): the node's
 // address is uniform, so its loads are scalar (SMEM) loads shared by the wave.
-template <bool STATS, bool CN, class STK, bool ROOT = false>
+template <bool STATS, int CN, class STK, bool ROOT = false>
 __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
   if (STATS) st.nodes++;
   uint32_t k0, k1, k2, k3;
@@ -543,18 +553,18 @@ __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, const STK
   trav_resolve(sc, t, k0 != kMissKey ? r0 : kNoRef, lds);
 }
 
-template <bool STATS, bool CN, class STK>
+template <bool STATS, int CN, class STK>
 __device__ __forceinline__ void root_step(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
   node_step<STATS, CN, STK, true>(sc, t, lds, st);
 }
 
 // Test the next triangle of the pending leaf; a lane without a node to visit
 // takes the next stack entry once its leaf is done.
-template <bool STATS, bool CN = false, class STK>
+template <bool STATS, int CN = 0, class STK>
 __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, const STK& lds,
                                          TravStats& st) {
   // 1/d: under CN t.inv holds s/d, and (s/d) * (1/s) is 1/d exactly
-  const f3 inv = CN ? sc.rcstep * t.inv : t.inv;
+  const f3 inv = CN ? rcstep_of<CN>(sc) * t.inv : t.inv;
 #if WGT_TRI_PER_STEP > 1
   // up to WGT_TRI_PER_STEP triangles of the open leaf per step, their loads issued together
   // (a slot past the leaf's end re-reads the first record and is ignored): the closest hit

@@ -151,14 +151,12 @@ constexpr int kLeafMax = 8;
 // measured faster than refs in a separate array (two lines per visit) or 128-B
 // records (the full footprint).
 constexpr int kCNodeFloats = 16;     // the node part, as exported by wgt_bvh_build_compact
-// WGT_CN64 (an A/B form): a 64-B record, the three code float4s then the four refs as
-// 24-bit fields whose top bytes hold the origin, org/s = 512 K per axis with K a signed
-// byte (host/bvh.cpp CompactNode64), decoded per visit instead of read as floats
-#ifdef WGT_CN64
-constexpr int kCRecordFloat4s = 4;
-#else
 constexpr int kCRecordFloat4s = 5;  // node + refs, the device record
-#endif
+// The 64-B form (WGT_CNODE=3): the three code float4s, then the four refs
+// as 24-bit fields whose top bytes hold the origin, org/s = 512 K per axis with K a signed
+// byte (host/bvh.cpp CompactNode64), decoded per visit instead of read as floats.  Its own
+// decode step (the 512-step origin grid widens the code range).
+constexpr int kC64RecordFloat4s = 4;
 constexpr size_t kCompactNodeBytes = (size_t)4 << 20;
 WGT_HD float qdec(float code, float step, float org) { return __builtin_fmaf(code, step, org); }
 WGT_HD float half_bits_to_float(uint32_t b) {

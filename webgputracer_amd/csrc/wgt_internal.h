@@ -47,6 +47,10 @@ struct DevScene {
   float cstep;                        // scene-wide decode step of the compact nodes (a power of two)
   float rcstep;                       // 1 / cstep
   float cbound;                       // the compact codes hold for ray origins with |coordinate| <= cbound
+  // the same tree as 64-B compact records (kC64RecordFloat4s, WGT_CNODE=3), their step and
+  // 1 / step; c64bound < 0 when the tree's refs or origins do not fit the form
+  const float4* __restrict__ cnodes64;
+  float c64step, rc64step, c64bound;
   uint32_t n_lights, n_quads, n_spheres, n_tris;
   uint32_t n_nodes;
   uint32_t last_sphere_emissive;
@@ -113,8 +117,9 @@ struct DevFrame {
   // speculative traversal: a triangle step runs when lanes with a pending leaf
   // number >= tri_ratio % of the lanes with a node to visit
   uint32_t tri_ratio;
-  // BVH node form of k_render_ps: 0 = 128-B nodes, 1 = compact nodes, 2 = compact
-  // when the 128-B tree exceeds kCompactNodeBytes (default)
+  // BVH node form of k_render_ps: 0 = 128-B nodes, 1 = 80-B compact records, 2 = 80-B
+  // compact records when the 128-B tree exceeds kCompactNodeBytes (default), 3 = 64-B
+  // compact records (node_form)
   uint32_t cnode;
   // persistent k_render_ps: pixel slots of the launch (64 per 8x8 block), the
   // idle lanes that trigger a refill from the pixel queue, LPT ordering (0 = off,
@@ -169,8 +174,9 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
                          uchar4* out8, float4* out32, uint32_t* outhit,
                          unsigned long long* counters, uint32_t resident, void* ws, size_t ws_cap,
                          hipStream_t stream);
-// Whether k_render_ps reads the compact node form for this scene and frame (DevFrame::cnode).
-bool use_compact_nodes(const DevScene& sc, const DevFrame& fr);
+// The node form k_render_ps reads for this scene and frame (DevFrame::cnode): 0 = 128-B
+// nodes, 1 = 80-B compact records, 2 = 64-B compact records.
+int node_form(const DevScene& sc, const DevFrame& fr);
 // Waves of k_render_ps resident on the whole device for this scene's LDS stack.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves);
 hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d_counts, hipStream_t stream);

@@ -111,7 +111,7 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
 // LDS words (Park) while the wave runs a service pass, and the LDS holds sc.ps_cap stack
 // entries per lane with the rest on a per-lane global stack (park_fix): the service code
 // then holds no traversal registers, which it used to spill to scratch.
-template <bool STATS, bool COST, bool CN, int W, bool TRIS = true, bool PK = false>
+template <bool STATS, bool COST, int CN, int W, bool TRIS = true, bool PK = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
@@ -493,7 +493,7 @@ hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d
 // tree would not fit one XCD's 4 MB L2 (sponza stand-in: 8.5 MB -> 4.3 + 1.1 MB);
 // a tree that fits keeps the 128-B nodes, whose step needs fewer VALU.
 // k_render_ps at the scene's waves per SIMD and node form.
-template <bool STATS, bool COST, bool CN, int W>
+template <bool STATS, bool COST, int CN, int W>
 void ps_launch_w(const DevScene& sc, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
                  const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
                  uint32_t* queue) {
@@ -502,27 +502,38 @@ void ps_launch_w(const DevScene& sc, dim3 grid, dim3 block, size_t lds, hipStrea
   else
     k_render_ps<STATS, COST, CN, W, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
 }
+// k_render_ps at the scene's waves per SIMD and the frame's node form (node_form); the
+// 64-B form is instantiated at 6 waves only (its 24-bit refs are those of Stack24 trees)
 template <bool STATS, bool COST>
-void ps_launch(const DevScene& sc, bool cn, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
+void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
                const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
                uint32_t* queue) {
   if (sc.n_tris == 0) {
-    k_render_ps<STATS, COST, false, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+    k_render_ps<STATS, COST, 0, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
   } else if (sc.ps_waves == 6) {
-    if (cn) ps_launch_w<STATS, COST, true, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
-    else ps_launch_w<STATS, COST, false, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    if (cn == 2) ps_launch_w<STATS, COST, 2, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    else if (cn == 1) ps_launch_w<STATS, COST, 1, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    else ps_launch_w<STATS, COST, 0, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
   } else {
-    if (cn) ps_launch_w<STATS, COST, true, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
-    else ps_launch_w<STATS, COST, false, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    if (cn) ps_launch_w<STATS, COST, 1, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    else ps_launch_w<STATS, COST, 0, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
   }
 }
 
-// The compact codes are exact for ray origins within sc.cbound (their margin, wgt_geom.h):
+// The compact codes are exact for ray origins within their bound (the margin, wgt_geom.h):
 // hit points always are, the camera is checked per frame (beyond: the 128-B nodes).
-bool use_compact_nodes(const DevScene& sc, const DevFrame& fr) {
+// WGT_CNODE: 0 = 128-B, 1 = 80-B, 2 = 80-B when the 128-B tree would not fit one XCD's
+// 4 MB L2 (sponza stand-in: 7.3 MB -> 4.6 MB; default), 3 = 64-B (at 6 waves per SIMD, when
+// the tree fits the form; else as 1).  A tree that fits keeps the 128-B nodes, whose step
+// needs fewer VALU.
+int node_form(const DevScene& sc, const DevFrame& fr) {
   const float cam = fmaxf(fmaxf(fabsf(fr.ox), fabsf(fr.oy)), fabsf(fr.oz));
-  if (!(cam <= sc.cbound)) return false;
-  return fr.cnode == 1 || (fr.cnode == 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes);
+  if (fr.cnode == 3 && sc.ps_waves == 6 && cam <= sc.c64bound) return 2;
+  if (!(cam <= sc.cbound)) return 0;
+  return fr.cnode == 1 || fr.cnode == 3 ||
+                 (fr.cnode == 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes)
+             ? 1
+             : 0;
 }
 
 // the parked kernel's global stacks: sc.stack entries per lane of every resident wave
@@ -557,7 +568,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
     // workspace (the context's, used in stream order): [0] pre-pass queue,
     // [1] queue | cost[nb] | perm[nb]
     const bool lpt = fr.pq_lpt && fr.sqrt_spp > fr.pq_lpt;
-    const bool cn = use_compact_nodes(sc, fr);
+    const int cn = node_form(sc, fr);
     uint32_t* q = (uint32_t*)ws;
     DevFrame f = fr;
     // phase thresholds swept per wave budget (profiles/sweeps/r01_sweep_compact_knobs.jsonl)
@@ -606,15 +617,15 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
 
 template <int W, bool PK>
 const void* ps_kernel(bool stats, bool cn) {
-  if (stats) return cn ? reinterpret_cast<const void*>(&k_render_ps<true, false, true, W, true, PK>)
-                       : reinterpret_cast<const void*>(&k_render_ps<true, false, false, W, true, PK>);
-  return cn ? reinterpret_cast<const void*>(&k_render_ps<false, false, true, W, true, PK>)
-            : reinterpret_cast<const void*>(&k_render_ps<false, false, false, W, true, PK>);
+  if (stats) return cn ? reinterpret_cast<const void*>(&k_render_ps<true, false, 1, W, true, PK>)
+                       : reinterpret_cast<const void*>(&k_render_ps<true, false, 0, W, true, PK>);
+  return cn ? reinterpret_cast<const void*>(&k_render_ps<false, false, 1, W, true, PK>)
+            : reinterpret_cast<const void*>(&k_render_ps<false, false, 0, W, true, PK>);
 }
 
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
-  const void* notris[2] = {reinterpret_cast<const void*>(&k_render_ps<false, false, false, kPsWavesNoTris, false>),
-                           reinterpret_cast<const void*>(&k_render_ps<true, false, false, kPsWavesNoTris, false>)};
+  const void* notris[2] = {reinterpret_cast<const void*>(&k_render_ps<false, false, 0, kPsWavesNoTris, false>),
+                           reinterpret_cast<const void*>(&k_render_ps<true, false, 0, kPsWavesNoTris, false>)};
   const void* variants[4];
   for (int i = 0; i < 4; ++i) {
     const bool stats = i & 1, cn = i >> 1;

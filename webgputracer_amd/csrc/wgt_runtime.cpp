@@ -154,6 +154,18 @@ uint32_t ps_waves_for(const BvhOut& bvh, uint32_t n_tris) {
   return bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris ? 6u : 5u;
 }
 
+// Whether the tree has the 64-B compact form (wgt_geom.h kC64RecordFloat4s): every node's
+// origin fits its grid byte (c64_ok) and every child ref its 24-bit field (internal refs
+// as byte offsets of 64-B records, leaf refs as they are).
+bool c64_fits(const BvhOut& bvh) {
+  if (!bvh.c64_ok || bvh.n_nodes == 0) return false;
+  for (int32_t r : bvh.crefs) {
+    const int64_t b = r >= 0 ? (int64_t)r * kC64RecordFloat4s * 16 : (int64_t)r;
+    if (b >= (1 << 23) || b < -(1 << 23)) return false;
+  }
+  return true;
+}
+
 // Parked traversal state of k_render_ps (WGT_PARK=0: the whole
 // stack in LDS): the LDS stack holds what fits beside the parked words at the wave budget,
 // or the whole stack (`stack` entries) when that is smaller; WGT_PS_CAP lowers it, down to
@@ -512,6 +524,7 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   info->bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
   info->bvh_compact_step = bvh.cstep;
   info->ps_waves = ps_waves_for(bvh, n_tris);
+  info->bvh_c64 = c64_fits(bvh) ? 1u : 0u;
   ps_park_cap(n_tris, (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u, info->ps_waves, info->ps_park,
               info->ps_stack);
   return WGT_OK;
@@ -567,32 +580,30 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const size_t b_nodes = align256(bvh.nodes.size() * 4);
   // compact records: the 64-B node followed by its 16-B refs (wgt_geom.h)
   std::vector<uint32_t> crec((size_t)bvh.n_nodes * kCRecordFloat4s * 4);
-#ifdef WGT_CN64
-  // the 64-B form: codes, then 24-bit refs (internal: byte offsets) under the origin bytes
-  bool c64 = bvh.c64_ok;
-  for (size_t i = 0; i < bvh.n_nodes; ++i) {
-    std::memcpy(&crec[i * 16], &bvh.c64[i * 16], 64);
-    for (int k = 0; k < 4; ++k) {
-      int64_t r = bvh.crefs[i * 4 + k];
-      if (r >= 0) r *= 64;
-      if (r >= (1 << 23) || r < -(1 << 23)) c64 = false;
-      crec[i * 16 + 12 + k] |= (uint32_t)r & 0xffffffu;
-    }
-  }
-  for (size_t i = 0; i < bvh.n_nodes; ++i)
-    for (int k = 0; k < 4; ++k) {
-#else
   for (size_t i = 0; i < bvh.n_nodes; ++i) {
     std::memcpy(&crec[i * kCRecordFloat4s * 4], &bvh.cnodes[i * kCNodeFloats], kCNodeFloats * 4);
     std::memcpy(&crec[i * kCRecordFloat4s * 4 + kCNodeFloats], &bvh.crefs[i * 4], 16);
   }
+  // the 64-B form (WGT_CNODE=3): codes, then 24-bit refs (internal: byte offsets) under the
+  // origin bytes; a tree whose refs or origins do not fit it has none (c64 = false)
+  bool c64 = c64_fits(bvh);
+  std::vector<uint32_t> c64rec(c64 ? (size_t)bvh.n_nodes * kC64RecordFloat4s * 4 : 0);
+  for (size_t i = 0; c64 && i < bvh.n_nodes; ++i) {
+    std::memcpy(&c64rec[i * 16], &bvh.c64[i * 16], 64);
+    for (int k = 0; k < 4; ++k) {
+      int64_t r = bvh.crefs[i * 4 + k];
+      if (r >= 0) r *= kC64RecordFloat4s * 16;
+      if (r >= (1 << 23) || r < -(1 << 23)) c64 = false;
+      c64rec[i * 16 + 12 + k] |= (uint32_t)r & 0xffffffu;
+    }
+  }
+  if (!c64) c64rec.clear();
   // device copies address child nodes by byte offset (one add to the uniform base in
   // the kernels instead of an index multiply); leaf refs are unchanged
   for (size_t i = 0; i < bvh.n_nodes; ++i)
     for (int k = 0; k < 4; ++k) {
       int32_t& r = reinterpret_cast<int32_t&>(crec[i * kCRecordFloat4s * 4 + kCNodeFloats + k]);
       if (r >= 0) r *= (int32_t)(kCRecordFloat4s * 16);
-#endif
       int32_t r128;
       std::memcpy(&r128, &bvh.nodes[i * kNode4Floats + 24 + k], 4);
       if (r128 >= 0) r128 *= (int32_t)(kNode4Floats * 4);
@@ -616,7 +627,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   }
   const size_t b_tris = align256(dtris.size() * 4);
   const size_t b_shade = align256(bvh.tshade.size() * 4);
-  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes;
+  const size_t b_c64 = align256(c64rec.size() * 4);
+  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64;
 
   {
     int rc = use_drain(ctx);  // no launch on any stream may still read the old scene
@@ -639,6 +651,9 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris, bvh.tshade.data(),
                 bvh.tshade.size() * 4);
     std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade, crec.data(), crec.size() * 4);
+    if (c64)
+      std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes, c64rec.data(),
+                  c64rec.size() * 4);
   }
   WGT_HIP(ctx, hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
 
@@ -650,13 +665,12 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.tris = (const float4*)(base + b_quads + b_sph + b_nodes);
   sc.tshade = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris);
   sc.cnodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade);
-#ifdef WGT_CN64
-  sc.cstep = bvh.c64step;
-  sc.cbound = c64 ? bvh.cbound : -1.0f;  // a tree the 64-B form cannot hold reads the 128-B nodes
-#else
+  sc.cnodes64 = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes);
   sc.cstep = bvh.cstep;
   sc.cbound = bvh.cbound;
-#endif
+  sc.c64step = bvh.c64step;
+  sc.rc64step = 1.0f / sc.c64step;  // a power of two: exact
+  sc.c64bound = c64 ? bvh.cbound : -1.0f;  // without the 64-B form, WGT_CNODE=3 reads the 80-B one
   sc.rcstep = 1.0f / sc.cstep;  // a power of two: exact
   sc.n_lights = n_lights;
   sc.n_quads = n_quads;
@@ -700,6 +714,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   in.ps_waves = n_tris ? sc.ps_waves : 0u;
   in.ps_park = sc.ps_park;
   in.ps_stack = n_tris ? sc.ps_cap : 0u;
+  in.bvh_c64 = c64 ? 1u : 0u;
   ctx->has_scene = true;
   return WGT_OK;
 }
