@@ -506,6 +506,15 @@ __device__ __forceinline__ uint32_t park_fix(const DevScene& sc, const Park& P, 
   if (sp + 4u > cap) {  // overflow: all but the top `keep` entries move to the global stack
     const uint32_t keep = (cap - 3u) / 2u;  // 1 <= keep <= cap - 4 for cap >= kMinPsCap
     const uint32_t m = sp - keep;
+    if (g + m > sc.stack) {
+      // g + sp never exceeds the builder's bound sc.stack (the global stack's size); were
+      // it to, the traversal ends here (a wrong image the parity tests catch) rather than
+      // writing out of bounds or spilling forever
+      P.st(8, (uint32_t)kNoRef);
+      P.st(10, 0u);
+      P.st(9, 0u);
+      return 3u;
+    }
     for (uint32_t i = 0; i < m; ++i) gs[(size_t)(g + i) * stride] = lds.ld((int)i);
     for (uint32_t i = 0; i < keep; ++i) lds.st((int)i, lds.ld((int)(i + m)));
     P.st(9, keep | (g + m) << 16);

@@ -120,6 +120,10 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   // 6 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
   using STK = typename std::conditional<W == 6, Stack24, Stack32>::type;
   const uint32_t cap = PK ? sc.ps_cap : sc.stack;  // LDS stack entries per lane
+  // PK: the highest stack top a node step may start from, cap - 4 (3 pushes and a parked
+  // leaf above it); no bound when the LDS holds the builder's whole stack (cap = sc.stack),
+  // which no traversal exceeds (and then no global stack exists, DevFrame::ps_spill)
+  const uint32_t top_max = PK && cap < sc.stack ? cap - 4u : 0xffffffffu;
   STK lds;
   Park P;
   if constexpr (W == 6) {
@@ -292,7 +296,9 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           // enter the traversal phase
           if (TRIS) {
             WGT_REGION(cr_root, root_step<STATS, CN>(sc, t, lds, st));
-            if (trav_done(t)) pending = true;
+            // PK: a root step that leaves fewer than 4 free LDS entries (an LDS stack of
+            // fewer than 8) is fixed up (park_fix) before the ray traverses
+            if (trav_done(t) || (PK && (uint32_t)t.sp > top_max)) pending = true;
             else trav = true;
             if (PK) {
               park_put(P, t);
@@ -338,7 +344,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           node_step<STATS, CN>(sc, t, lds, st);
           // PK: fewer than 4 free LDS entries above the top (only node steps push): the
           // lane parks its state and leaves as if done; its service pass spills (park_fix)
-          if (PK && (uint32_t)t.sp + 4u > cap) {
+          if (PK && (uint32_t)t.sp > top_max) {
             park_put(P, t);
             parked = true;
             t.ref = kNoRef;
