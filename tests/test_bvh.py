@@ -234,12 +234,12 @@ def test_wave_budget_and_narrow_tree(monkeypatch):
         # the parked kernel keeps 20 of the 32 entries in LDS at 6 waves (3 B each beside 11
         # parked words: 13 x 512 B per wave), the 64-B compact form fits both trees
         assert info["ps_park"] == 1 and info["ps_stack"] == 20 and info["bvh_c64"] == 1
-    monkeypatch.setenv("WGT_PS_CAP", "7")
+    monkeypatch.setenv("WGT_PS_CAP", "11")
     info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
-    assert info["ps_stack"] == 7
+    assert info["ps_stack"] == 11
     monkeypatch.setenv("WGT_PS_CAP", "2")  # clamped to kMinPsCap
     info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
-    assert info["ps_stack"] == 5
+    assert info["ps_stack"] == 8
     monkeypatch.setenv("WGT_PARK", "0")
     info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
     assert info["ps_park"] == 0 and info["ps_stack"] == info["bvh_stack"] + 1

@@ -338,11 +338,11 @@ _SCHED_REF = {}
                                  # parked traversal state with the smallest LDS stack (every node
                                  # step near the top spills to the global stack), per node form and
                                  # wave budget; and the whole stack in LDS (WGT_PARK=0)
-                                 {"WGT_PS_CAP": "5"}, {"WGT_PS_CAP": "5", "WGT_CNODE": "1"},
-                                 {"WGT_PS_CAP": "6", "WGT_PS_WAVES": "5"}, {"WGT_PS_CAP": "9", "WGT_PQ_LPT": "0"},
+                                 {"WGT_PS_CAP": "8"}, {"WGT_PS_CAP": "8", "WGT_CNODE": "1"},
+                                 {"WGT_PS_CAP": "8", "WGT_PS_WAVES": "5"}, {"WGT_PS_CAP": "9", "WGT_PQ_LPT": "0"},
                                  {"WGT_PARK": "0"}, {"WGT_PARK": "0", "WGT_CNODE": "1"},
                                  # the 64-B compact records (runtime-selected since round 4)
-                                 {"WGT_CNODE": "3"}, {"WGT_CNODE": "3", "WGT_PS_CAP": "5"},
+                                 {"WGT_CNODE": "3"}, {"WGT_CNODE": "3", "WGT_PS_CAP": "8"},
                                  {"WGT_CNODE": "3", "WGT_PARK": "0"},
                                  ])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
@@ -371,10 +371,11 @@ def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     check_counters(g["stats"], r["counters"], oracle)
 
 
-@pytest.mark.parametrize("cap,cnode", [("5", "2"), ("5", "1"), ("7", "2")])
+@pytest.mark.parametrize("cap,cnode", [("8", "2"), ("8", "1"), ("8", "3"), ("11", "2")])
 def test_stack_overflow_spill_and_refill(ctx, wgt, oracle, bunny, cap, cnode, monkeypatch):
-    """The parked kernel's LDS stack bounded at 5 (or 7) entries (WGT_PS_CAP, the builder's
-    bound is 31): node steps that leave fewer than 4 free entries park the lane, whose
+    """The parked kernel's LDS stack bounded at 8 (or 11) entries (WGT_PS_CAP; the builder's
+    bound is 31, a node step may start only from a top <= 4 = 8 - 4, the 4-entry bound
+    round 3's review asked for): node steps that leave fewer than 4 free entries park the lane, whose
     service pass moves the bottom of its stack to the global stack, and a lane whose LDS
     part runs empty refills from it (park_fix).  Both paths must
     run (the counters) and the frame stay bit-exact against the oracle."""

@@ -71,8 +71,10 @@ constexpr uint32_t kStack24Tris = 1u << 20;   // leaf refs ~(first << 3 | count 
 // best index, node ref, stack top | global depth << 16, open leaf (offset | count)
 constexpr uint32_t kParkWords = 11;
 // The smallest LDS stack the parked kernel runs with: a node step needs 4 free entries
-// above the top (3 pushes and a parked leaf) and the top must keep one
-constexpr uint32_t kMinPsCap = 5;
+// above the top (3 pushes and a parked leaf), and a ray's root step, which pushes at most
+// 4, must leave its top within that bound (top <= cap - 4), so a new ray never starts
+// past it
+constexpr uint32_t kMinPsCap = 8;
 // Dynamic LDS bytes of a traversal kernel launch (4-byte entries).
 inline size_t stack_lds_bytes(const DevScene& sc) { return (size_t)sc.stack * kBlock * sizeof(int); }
 // ... of a k_render_ps launch: 3-byte entries at 6 waves per SIMD, ps_cap entries and

@@ -296,14 +296,14 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           // enter the traversal phase
           if (TRIS) {
             WGT_REGION(cr_root, root_step<STATS, CN>(sc, t, lds, st));
-            // PK: a root step that leaves fewer than 4 free LDS entries (an LDS stack of
-            // fewer than 8) is fixed up (park_fix) before the ray traverses
-            if (trav_done(t) || (PK && (uint32_t)t.sp > top_max)) pending = true;
-            else trav = true;
             if (PK) {
               park_put(P, t);
               P.st(9, (uint32_t)t.sp);  // a new ray's global stack is empty
             }
+            // (PK: a root step pushes at most 4 entries, and the LDS stack holds >= kMinPsCap
+            // = 8, so the ray starts its traversal with a top <= top_max)
+            if (trav_done(t)) pending = true;
+            else trav = true;
           } else {
             pending = true;  // no triangles: the quad and sphere scans are the whole query
           }
@@ -325,6 +325,9 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       const uint32_t sparse = (live * fr.ps_svc_frac) >> 6;
       to_service = sparse < to_service ? sparse : to_service;
     }
+    // PK: every lane takes its state from Park; a lane that is not traversing holds a
+    // finished one (a lane parked on its LDS bound is served before the next traversal
+    // phase: the first iteration of a service phase serves every lane that needs it)
     if (PK && TRIS) park_get(P, t);
     bool parked = false;  // PK: the lane left on its LDS stack bound, its state parked as it was
     for (; TRIS;) {
