@@ -231,9 +231,9 @@ def test_wave_budget_and_narrow_tree(monkeypatch):
         info, _, _ = w.bvh_build(w.procedural_mesh(kind))
         assert info["ps_waves"] == 6 and info["bvh_nodes"] < 1 << 16
         assert 25 < info["bvh_stack"] <= 31
-        # the parked kernel keeps 20 of the 32 entries in LDS at 6 waves (3 B each beside 11
-        # parked words: 13 x 512 B per wave), the 64-B compact form fits both trees
-        assert info["ps_park"] == 1 and info["ps_stack"] == 20 and info["bvh_c64"] == 1
+        # the parked kernel keeps 18 of the 32 entries in LDS at 6 waves (3 B each beside 11
+        # parked words: 6,400 B per wave, kPsLdsPerCu), the 64-B compact form fits both trees
+        assert info["ps_park"] == 1 and info["ps_stack"] == 18 and info["bvh_c64"] == 1
     monkeypatch.setenv("WGT_PS_CAP", "11")
     info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
     assert info["ps_stack"] == 11

@@ -283,7 +283,7 @@ def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, cnode, monkeypa
     info = ctx.scene_info()
     if not any(os.environ.get(k) for k in ("WGT_CNODE", "WGT_PS_WAVES", "WGT_STACK_LIMIT", "WGT_PARK")):
         assert (info["bvh_compact"], info["ps_waves"]) == ((1, 6) if kind == "sponza" else (0, 6))
-        assert info["ps_park"] == 1 and info["ps_stack"] == min(20, info["bvh_stack"] + 1)
+        assert info["ps_park"] == 1 and info["ps_stack"] == min(18, info["bvh_stack"] + 1)
     g = ctx.render_tile(wgt.camera_param(16 / 9, spp, 3), 1920, 1080, stats=True)
     if kind not in _FULL:
         osc = oracle.OracleScene(L, Q, S, T)

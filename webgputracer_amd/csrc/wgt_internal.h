@@ -84,10 +84,15 @@ inline size_t ps_stack_lds_bytes(const DevScene& sc) {
   if (sc.ps_park) return (size_t)sc.ps_cap * kBlock * entry + (size_t)kParkWords * kBlock * 4;
   return (size_t)sc.stack * kBlock * entry;
 }
-// LDS entries the parked kernel can hold at its wave budget: the stack and the parked
-// words of 4 * waves waves per CU within 13 (6 waves) / 16 (5 waves) x 512 B per wave
+// LDS entries the parked kernel can hold at its wave budget: the stack and the parked words
+// of 4 * waves one-wave workgroups per CU within kPsLdsPerCu.  Measured (profiles/r04/
+// lds_sweep_*.jsonl): 24 workgroups per CU run at full speed with 6,272 B each and lose 8-20 %
+// from 6,464 B on, although the occupancy API still reports 24 (and 160 KiB would hold 24 of
+// 6,656 B): the usable budget lies between 24 x 6,400 and 24 x 6,656 B, so 150 KiB is taken
+// (6 waves: 18 entries of 3 B beside the 11 parked words; 5 waves: 19 of 4 B)
+constexpr size_t kPsLdsPerCu = 150 * 1024;
 inline uint32_t ps_cap_max(uint32_t waves) {
-  const size_t per_wave = waves == 6 ? 13 * 512 : 16 * 512, entry = waves == 6 ? 3 : 4;
+  const size_t per_wave = kPsLdsPerCu / (4 * waves), entry = waves == 6 ? 3 : 4;
   return (uint32_t)((per_wave - (size_t)kParkWords * kBlock * 4) / (kBlock * entry));
 }
 

@@ -115,7 +115,11 @@ template <bool STATS, bool COST, int CN, int W, bool TRIS = true, bool PK = fals
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
-            unsigned long long* __restrict__ counters, uint32_t* __restrict__ queue) {
+            unsigned long long* __restrict__ counters, uint32_t* __restrict__ queue,
+            int* __restrict__ spill) {
+  // spill: the global stacks (PK, DevFrame::ps_spill), a kernel argument of its own: a
+  // noalias pointer, so its stores do not clobber the scene for the compiler, whose
+  // wave-uniform loads (quads, spheres, the root node) stay scalar loads
   extern __shared__ int s_stack[];  // stack entries per lane (+ parked words), ps_stack_lds_bytes
   // 6 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
   using STK = typename std::conditional<W == 6, Stack24, Stack32>::type;
@@ -228,7 +232,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           resume = (int)P.ld(8) != kNoRef || (P.ld(10) & 63u) != 0u || P.ld(9) != 0u;
           if (resume) {
             // the lane's global stack: entry e at gs[e * fr.ps_spill_stride]
-            const uint32_t k = park_fix(sc, P, lds, cap, fr.ps_spill + blockIdx.x * kBlock + lane, fr.ps_spill_stride);
+            const uint32_t k = park_fix(sc, P, lds, cap, spill + blockIdx.x * kBlock + lane, fr.ps_spill_stride);
             if (STATS) {
               st.spills += k == 1u ? 1u : 0u;
               st.refills += k == 2u ? 1u : 0u;
@@ -265,7 +269,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           pending = false;
         }
         // start the next ray of this pixel
-        for (; !resume;) {
+        if (!resume) for (;;) {
           if (px_done(fr, px)) {
             have = false;
             fin = true;
@@ -507,9 +511,9 @@ void ps_launch_w(const DevScene& sc, dim3 grid, dim3 block, size_t lds, hipStrea
                  const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
                  uint32_t* queue) {
   if (sc.ps_park)
-    k_render_ps<STATS, COST, CN, W, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+    k_render_ps<STATS, COST, CN, W, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
   else
-    k_render_ps<STATS, COST, CN, W, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+    k_render_ps<STATS, COST, CN, W, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
 }
 // k_render_ps at the scene's waves per SIMD and the frame's node form (node_form); the
 // 64-B form is instantiated at 6 waves only (its 24-bit refs are those of Stack24 trees)
@@ -518,7 +522,7 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
                const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
                uint32_t* queue) {
   if (sc.n_tris == 0) {
-    k_render_ps<STATS, COST, 0, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
+    k_render_ps<STATS, COST, 0, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
   } else if (sc.ps_waves == 6) {
     if (cn == 2) ps_launch_w<STATS, COST, 2, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
     else if (cn == 1) ps_launch_w<STATS, COST, 1, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
