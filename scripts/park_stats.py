@@ -12,7 +12,7 @@ import webgputracer_amd as w  # noqa: E402
 for kind in ("sponza", "bunny"):
     scene = w.mesh_scene(kind)
     ctx = w.Context(0)
-    for cap in ("", "16", "12", "8"):
+    for cap in ("", "12", "8"):
         if cap:
             os.environ["WGT_PS_CAP"] = cap
         else:

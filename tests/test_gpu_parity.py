@@ -270,14 +270,16 @@ def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
 _FULL = {}
 
 
-@pytest.mark.parametrize("kind,spp,cnode", [("sponza", 4, None), ("sponza", 4, "3"), ("bunny", 1, None)])
-def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, cnode, monkeypatch):
+@pytest.mark.parametrize("kind,spp,env", [("sponza", 4, {}), ("sponza", 4, {"WGT_CNODE": "3"}),
+                                          ("sponza", 4, {"WGT_PS_WAVES": "7"}), ("bunny", 1, {})])
+def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatch):
     """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
     oracle (OpenMP), through the default kernel of each scene: sponza on the 80-B compact
     records, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries and
-    parked traversal state; and sponza on the 64-B compact records (WGT_CNODE=3)."""
-    if cnode is not None:
-        monkeypatch.setenv("WGT_CNODE", cnode)
+    parked traversal state; and sponza on the 64-B compact records (WGT_CNODE=3) and at 7
+    waves/SIMD (WGT_PS_WAVES=7, parked state, a 13-entry LDS stack)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     L, Q, S, T = wgt.mesh_scene(kind)
     ctx.upload_scene(L, Q, S, T)
     info = ctx.scene_info()
@@ -344,6 +346,9 @@ _SCHED_REF = {}
                                  # the 64-B compact records (runtime-selected since round 4)
                                  {"WGT_CNODE": "3"}, {"WGT_CNODE": "3", "WGT_PS_CAP": "8"},
                                  {"WGT_CNODE": "3", "WGT_PARK": "0"},
+                                 # 7 waves per SIMD (parked state only)
+                                 {"WGT_PS_WAVES": "7"}, {"WGT_PS_WAVES": "7", "WGT_CNODE": "1"},
+                                 {"WGT_PS_WAVES": "7", "WGT_CNODE": "3", "WGT_PS_CAP": "8"},
                                  ])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the

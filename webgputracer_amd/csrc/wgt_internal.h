@@ -80,7 +80,7 @@ inline size_t stack_lds_bytes(const DevScene& sc) { return (size_t)sc.stack * kB
 // ... of a k_render_ps launch: 3-byte entries at 6 waves per SIMD, ps_cap entries and
 // the parked state when ps_park
 inline size_t ps_stack_lds_bytes(const DevScene& sc) {
-  const size_t entry = sc.ps_waves == 6 ? 3 : sizeof(int);
+  const size_t entry = sc.ps_waves >= 6 ? 3 : sizeof(int);
   if (sc.ps_park) return (size_t)sc.ps_cap * kBlock * entry + (size_t)kParkWords * kBlock * 4;
   return (size_t)sc.stack * kBlock * entry;
 }
@@ -89,10 +89,10 @@ inline size_t ps_stack_lds_bytes(const DevScene& sc) {
 // lds_sweep_*.jsonl): 24 workgroups per CU run at full speed with 6,272 B each and lose 8-20 %
 // from 6,464 B on, although the occupancy API still reports 24 (and 160 KiB would hold 24 of
 // 6,656 B): the usable budget lies between 24 x 6,400 and 24 x 6,656 B, so 150 KiB is taken
-// (6 waves: 18 entries of 3 B beside the 11 parked words; 5 waves: 19 of 4 B)
+// (6 waves: 18 entries of 3 B beside the 11 parked words; 7 waves: 13 of 3 B; 5 waves: 19 of 4 B)
 constexpr size_t kPsLdsPerCu = 150 * 1024;
 inline uint32_t ps_cap_max(uint32_t waves) {
-  const size_t per_wave = kPsLdsPerCu / (4 * waves), entry = waves == 6 ? 3 : 4;
+  const size_t per_wave = kPsLdsPerCu / (4 * waves), entry = waves >= 6 ? 3 : 4;
   return (uint32_t)((per_wave - (size_t)kParkWords * kBlock * 4) / (kBlock * entry));
 }
 

@@ -121,8 +121,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   // noalias pointer, so its stores do not clobber the scene for the compiler, whose
   // wave-uniform loads (quads, spheres, the root node) stay scalar loads
   extern __shared__ int s_stack[];  // stack entries per lane (+ parked words), ps_stack_lds_bytes
-  // 6 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
-  using STK = typename std::conditional<W == 6, Stack24, Stack32>::type;
+  // 6 or 7 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
+  using STK = typename std::conditional<W >= 6, Stack24, Stack32>::type;
   const uint32_t cap = PK ? sc.ps_cap : sc.stack;  // LDS stack entries per lane
   // PK: the highest stack top a node step may start from, cap - 4 (3 pushes and a parked
   // leaf above it); no bound when the LDS holds the builder's whole stack (cap = sc.stack),
@@ -130,7 +130,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   const uint32_t top_max = PK && cap < sc.stack ? cap - 4u : 0xffffffffu;
   STK lds;
   Park P;
-  if constexpr (W == 6) {
+  if constexpr (W >= 6) {
     lds.lo = (uint16_t*)s_stack + threadIdx.x;
     lds.hi = (int8_t*)((uint16_t*)s_stack + cap * kBlock) + threadIdx.x;
     P.p = (uint32_t*)((char*)s_stack + cap * kBlock * 3) + threadIdx.x;
@@ -523,6 +523,10 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
                uint32_t* queue) {
   if (sc.n_tris == 0) {
     k_render_ps<STATS, COST, 0, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
+  } else if (sc.ps_waves == 7) {  // parked state only (the whole stack does not fit LDS at 7)
+    if (cn == 2) k_render_ps<STATS, COST, 2, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
+    else if (cn == 1) k_render_ps<STATS, COST, 1, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
+    else k_render_ps<STATS, COST, 0, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
   } else if (sc.ps_waves == 6) {
     if (cn == 2) ps_launch_w<STATS, COST, 2, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
     else if (cn == 1) ps_launch_w<STATS, COST, 1, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
@@ -541,7 +545,7 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
 // needs fewer VALU.
 int node_form(const DevScene& sc, const DevFrame& fr) {
   const float cam = fmaxf(fmaxf(fabsf(fr.ox), fabsf(fr.oy)), fabsf(fr.oz));
-  if (fr.cnode == 3 && sc.ps_waves == 6 && cam <= sc.c64bound) return 2;
+  if (fr.cnode == 3 && sc.ps_waves >= 6 && cam <= sc.c64bound) return 2;
   if (!(cam <= sc.cbound)) return 0;
   return fr.cnode == 1 || fr.cnode == 3 ||
                  (fr.cnode == 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes)
@@ -585,8 +589,8 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
     uint32_t* q = (uint32_t*)ws;
     DevFrame f = fr;
     // phase thresholds swept per wave budget (profiles/sweeps/r01_sweep_compact_knobs.jsonl)
-    if (f.ps_to_trav == 0) f.ps_to_trav = sc.ps_waves == 6 ? 16u : 18u;
-    if (f.ps_to_service == 0) f.ps_to_service = sc.ps_waves == 6 ? 14u : 16u;
+    if (f.ps_to_trav == 0) f.ps_to_trav = sc.ps_waves >= 6 ? 16u : 18u;
+    if (f.ps_to_service == 0) f.ps_to_service = sc.ps_waves >= 6 ? 14u : 16u;
     if (f.pq_refill == 0) f.pq_refill = 2u;
     f.n_slots = nb * 64u;
     f.perm = nullptr;
@@ -642,7 +646,8 @@ hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
   const void* variants[4];
   for (int i = 0; i < 4; ++i) {
     const bool stats = i & 1, cn = i >> 1;
-    if (sc.ps_waves == 6) variants[i] = sc.ps_park ? ps_kernel<6, true>(stats, cn) : ps_kernel<6, false>(stats, cn);
+    if (sc.ps_waves == 7) variants[i] = ps_kernel<7, true>(stats, cn);
+    else if (sc.ps_waves == 6) variants[i] = sc.ps_park ? ps_kernel<6, true>(stats, cn) : ps_kernel<6, false>(stats, cn);
     else variants[i] = sc.ps_park ? ps_kernel<5, true>(stats, cn) : ps_kernel<5, false>(stats, cn);
   }
   // the largest of the variants' capacities: waves beyond a variant's capacity

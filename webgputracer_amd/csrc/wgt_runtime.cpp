@@ -150,8 +150,12 @@ uint32_t ps_waves_for(const BvhOut& bvh, uint32_t n_tris) {
   // no triangles: the kernel without traversal (4-byte stack bytes in the launch and
   // the occupancy query alike, ps_stack_lds_bytes)
   if (n_tris == 0) return (uint32_t)kPsWavesNoTris;
-  if (env_u32("WGT_PS_WAVES", 0) == 5) return 5u;
-  return bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris ? 6u : 5u;
+  const uint32_t forced = env_u32("WGT_PS_WAVES", 0);
+  if (forced == 5) return 5u;
+  const bool fits24 = bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris;
+  // 7 waves per SIMD (72 VGPRs) exist with the parked state only (WGT_PS_WAVES=7)
+  if (forced == 7 && fits24 && env_u32("WGT_PARK", 1)) return 7u;
+  return fits24 ? 6u : 5u;
 }
 
 // Whether the tree has the 64-B compact form (wgt_geom.h kC64RecordFloat4s): every node's
