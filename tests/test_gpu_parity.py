@@ -271,13 +271,14 @@ _FULL = {}
 
 
 @pytest.mark.parametrize("kind,spp,env", [("sponza", 4, {}), ("sponza", 4, {"WGT_CNODE": "3"}),
-                                          ("sponza", 4, {"WGT_PS_WAVES": "7"}), ("bunny", 1, {})])
+                                          ("sponza", 4, {"WGT_PARK": "1"}), ("sponza", 4, {"WGT_PS_WAVES": "7"}),
+                                          ("bunny", 1, {})])
 def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatch):
     """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
     oracle (OpenMP), through the default kernel of each scene: sponza on the 80-B compact
-    records, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries and
-    parked traversal state; and sponza on the 64-B compact records (WGT_CNODE=3) and at 7
-    waves/SIMD (WGT_PS_WAVES=7, parked state, a 13-entry LDS stack)."""
+    records, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries; and
+    sponza on the 64-B compact records (WGT_CNODE=3), with parked traversal state (WGT_PARK=1,
+    an 18-entry LDS stack) and at 7 waves/SIMD (WGT_PS_WAVES=7, parked, 13 entries)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     L, Q, S, T = wgt.mesh_scene(kind)
@@ -285,7 +286,7 @@ def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatc
     info = ctx.scene_info()
     if not any(os.environ.get(k) for k in ("WGT_CNODE", "WGT_PS_WAVES", "WGT_STACK_LIMIT", "WGT_PARK")):
         assert (info["bvh_compact"], info["ps_waves"]) == ((1, 6) if kind == "sponza" else (0, 6))
-        assert info["ps_park"] == 1 and info["ps_stack"] == min(18, info["bvh_stack"] + 1)
+        assert info["ps_park"] == 0 and info["ps_stack"] == info["bvh_stack"] + 1
     g = ctx.render_tile(wgt.camera_param(16 / 9, spp, 3), 1920, 1080, stats=True)
     if kind not in _FULL:
         osc = oracle.OracleScene(L, Q, S, T)
@@ -337,15 +338,15 @@ _SCHED_REF = {}
                                  {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
                                  {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}, {"WGT_NARROW": "1"},
                                  {"WGT_STACK_LIMIT": "20"},
-                                 # parked traversal state with the smallest LDS stack (every node
-                                 # step near the top spills to the global stack), per node form and
-                                 # wave budget; and the whole stack in LDS (WGT_PARK=0)
-                                 {"WGT_PS_CAP": "8"}, {"WGT_PS_CAP": "8", "WGT_CNODE": "1"},
-                                 {"WGT_PS_CAP": "8", "WGT_PS_WAVES": "5"}, {"WGT_PS_CAP": "9", "WGT_PQ_LPT": "0"},
-                                 {"WGT_PARK": "0"}, {"WGT_PARK": "0", "WGT_CNODE": "1"},
+                                 # parked traversal state (WGT_PARK=1): the default LDS stack, the
+                                 # smallest (every node step near the top spills to the global stack),
+                                 # per node form and wave budget
+                                 {"WGT_PARK": "1"}, {"WGT_PARK": "1", "WGT_CNODE": "1"},
+                                 {"WGT_PARK": "1", "WGT_PS_CAP": "8"}, {"WGT_PARK": "1", "WGT_PS_CAP": "8", "WGT_CNODE": "1"},
+                                 {"WGT_PARK": "1", "WGT_PS_CAP": "8", "WGT_PS_WAVES": "5"},
+                                 {"WGT_PARK": "1", "WGT_PS_CAP": "9", "WGT_PQ_LPT": "0"},
                                  # the 64-B compact records (runtime-selected since round 4)
-                                 {"WGT_CNODE": "3"}, {"WGT_CNODE": "3", "WGT_PS_CAP": "8"},
-                                 {"WGT_CNODE": "3", "WGT_PARK": "0"},
+                                 {"WGT_CNODE": "3"}, {"WGT_CNODE": "3", "WGT_PARK": "1", "WGT_PS_CAP": "8"},
                                  # 7 waves per SIMD (parked state only)
                                  {"WGT_PS_WAVES": "7"}, {"WGT_PS_WAVES": "7", "WGT_CNODE": "1"},
                                  {"WGT_PS_WAVES": "7", "WGT_CNODE": "3", "WGT_PS_CAP": "8"},
@@ -357,7 +358,7 @@ def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     wave budget: 6 waves per SIMD with 3-byte stack entries or, with WGT_PS_WAVES=5, 5
     with 4-byte ones; the narrow 25-entry tree, WGT_NARROW=1; a 20-entry bound, which moves
     the 3-byte stack's byte array; the parked traversal state with small LDS stacks,
-    WGT_PS_CAP, and the whole stack in LDS, WGT_PARK=0)
+    WGT_PARK=1 with LDS stacks down to WGT_PS_CAP=8; 7 waves per SIMD)
     change which lane renders which pixel and when, never a bit of the result.  100x60
     leaves ragged 8x8 blocks at the frame edge.  The test runs after the kernel-family
     tests on the same context, the sequence that exposed a workspace-reuse bug (each
@@ -385,6 +386,7 @@ def test_stack_overflow_spill_and_refill(ctx, wgt, oracle, bunny, cap, cnode, mo
     part runs empty refills from it (park_fix).  Both paths must
     run (the counters) and the frame stay bit-exact against the oracle."""
     (L, Q, S, T), osc = bunny
+    monkeypatch.setenv("WGT_PARK", "1")
     monkeypatch.setenv("WGT_PS_CAP", cap)
     monkeypatch.setenv("WGT_CNODE", cnode)
     ctx.upload_scene(L, Q, S, T)

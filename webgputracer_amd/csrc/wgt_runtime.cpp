@@ -153,8 +153,8 @@ uint32_t ps_waves_for(const BvhOut& bvh, uint32_t n_tris) {
   const uint32_t forced = env_u32("WGT_PS_WAVES", 0);
   if (forced == 5) return 5u;
   const bool fits24 = bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris;
-  // 7 waves per SIMD (72 VGPRs) exist with the parked state only (WGT_PS_WAVES=7)
-  if (forced == 7 && fits24 && env_u32("WGT_PARK", 1)) return 7u;
+  // 7 waves per SIMD (72 VGPRs) exist with the parked state only (WGT_PS_WAVES=7 parks)
+  if (forced == 7 && fits24) return 7u;
   return fits24 ? 6u : 5u;
 }
 
@@ -170,12 +170,13 @@ bool c64_fits(const BvhOut& bvh) {
   return true;
 }
 
-// Parked traversal state of k_render_ps (WGT_PARK=0: the whole
-// stack in LDS): the LDS stack holds what fits beside the parked words at the wave budget,
+// Parked traversal state of k_render_ps (opt-in: WGT_PARK=1; it
+// removes the service phase's scratch stores but measured 5 % slower, profiles/r04/): the LDS
+// stack holds what fits beside the parked words at the wave budget,
 // or the whole stack (`stack` entries) when that is smaller; WGT_PS_CAP lowers it, down to
 // kMinPsCap, for tests.
 void ps_park_cap(uint32_t n_tris, uint32_t stack, uint32_t waves, uint32_t& park, uint32_t& cap) {
-  park = n_tris > 0 && env_u32("WGT_PARK", 1) ? 1u : 0u;
+  park = n_tris > 0 && (env_u32("WGT_PARK", 0) || env_u32("WGT_PS_WAVES", 0) == 7) ? 1u : 0u;
   cap = stack;
   if (!park) return;
   uint32_t c = std::min(stack, ps_cap_max(waves));
