@@ -63,7 +63,7 @@ __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict_
   if (fabs_w(denom) < kRayMin) return;
   const float4 wd = q[4];
   const float num = wd.w - dot(qn, o);
-  if (quad_t_negative(num, denom)) return;
+  if (WGT_QUAD_SIGN && quad_t_negative(num, denom)) return;
   const float t = EXACT ? num / denom : div_rn(num, denom);
   if (t < kRayMin || kRayMax < t) return;
   // ray_dist is monotone non-decreasing in t >= 0 (each rounded step is), so t >=
@@ -135,7 +135,7 @@ __device__ __forceinline__ void isect_quad_axis(f3 o, f3 d, const float4* __rest
   const float denom = s * comp<K>(d);
   if (fabs_w(denom) < kRayMin) return;
   const float num = q[4].w - s * comp<K>(o);
-  if (quad_t_negative(num, denom)) return;
+  if (WGT_QUAD_SIGN && quad_t_negative(num, denom)) return;
   const float t = div_rn(num, denom);
   if (t < kRayMin || kRayMax < t) return;
   if (t >= qt) return;  // see isect_quad
