@@ -204,7 +204,7 @@ int wgt_render_frames(wgt_ctx *ctx, const wgt_camera_param *cam, uint32_t W, uin
  * cam->seed is ignored (per-tile seeds).  Always asynchronous: the call returns
  * as soon as the launches are queued, ordered on `stream`; read the outputs only
  * after synchronising `stream`.  The context's launches use its scheduling
- * workspaces round-robin (2 by default, WGT_WS_SLOTS = 1..4), and a launch waits
+ * workspaces round-robin (4 by default, WGT_WS_SLOTS = 1..4), and a launch waits
  * on the device only for the previous launch that used the same workspace: two
  * consecutive calls on different streams may run concurrently (the next frame's
  * waves fill the CUs the previous frame's end-of-launch drain leaves idle), so the

@@ -7,12 +7,20 @@ samples are a serial RNG chain, path_tracer.wgsl:378, 381-395) at 1/N of the wor
   efficiency(N) = T_full / (N * max_r T_r)
 is what N ranks of the real job would reach without the gather (which adds ~1 MB per peer).
 
-  python scripts/strong_projection.py [--scene sponza] [--reps 2] [--ns 2 4 8] > out.jsonl
+--frames K --pipeline P: a job of K frames instead, each split over the N GPUs (bench.py
+--scaling strong): rank r renders its share of frame k on the context's pipeline stream k % P,
+P frames in flight, timed from the first launch to the last one's end (host clock between two
+device synchronisations), so a rank pays one drain per job instead of one per frame.  At N = 8
+a rank's share of a 1080p frame (259k pixels) is fewer pixels than the device holds lanes
+(6144 waves x 64), which P frames in flight make up for.
+
+  python scripts/strong_projection.py [--scene sponza] [--reps 2] [--ns 2 4 8] [--frames 8 --pipeline 4]
 """
 import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -29,6 +37,8 @@ def main():
     ap.add_argument("--tile", type=int, default=32)
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--ns", type=int, nargs="+", default=[2, 4, 8])
+    ap.add_argument("--frames", type=int, default=1, help="frames per job (1: one launch per rank, alone)")
+    ap.add_argument("--pipeline", type=int, default=1, help="frames in flight (1..4) when --frames > 1")
     a = ap.parse_args()
     import torch
 
@@ -59,15 +69,46 @@ def main():
                 best = ms if best is None else min(best, ms)
         return best
 
+    def timed_job(rank, n):
+        P = max(1, min(a.pipeline, 4))
+        streams = [ctx.pipeline_stream(i) for i in range(P)]
+        d_ts = [torch.from_numpy(wd.shard_tiles(W, H, T, [(k, k + 1)], rank, n).view(np.uint8).copy()).to(dev)
+                for k in range(a.frames)]
+        nt = len(d_ts[0]) // wd.TILE_DTYPE.itemsize
+        outs = [torch.zeros((nt, T, T, 4), dtype=torch.uint8, device=dev) for _ in range(P)]
+        best = None
+        for rep in range(a.reps + 1):  # the first job warms up
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for k, d_t in enumerate(d_ts):
+                ctx.render_tiles_async(cam, W, H, T, T, d_t.data_ptr(), nt, d_u8=outs[k % P].data_ptr(),
+                                       stream=streams[k % P])
+            torch.cuda.synchronize()
+            ms = (time.perf_counter() - t0) * 1e3 / a.frames
+            if rep > 0:
+                best = ms if best is None else min(best, ms)
+        return best
+
+    if a.frames > 1:
+        full = timed_job(0, 1)
+        base = {"scene": a.scene, "frames": a.frames, "pipeline": a.pipeline, "build_id": w.build_id()}
+        print(json.dumps({**base, "n": 1, "rank_ms_per_frame": [round(full, 3)], "efficiency": 1.0}), flush=True)
+        for n in a.ns:
+            ms = [timed_job(r, n) for r in range(n)]
+            print(json.dumps({**base, "n": n, "rank_ms_per_frame": [round(x, 3) for x in ms],
+                              "full_ms_per_frame": round(full, 3), "max_rank_ms_per_frame": round(max(ms), 3),
+                              "efficiency": round(full / (n * max(ms)), 4)}), flush=True)
+        ctx.close()
+        return
+
     full = timed(wd.shard_tiles(W, H, T, [(0, 0)], 0, 1))
     print(json.dumps({"scene": a.scene, "n": 1, "rank_ms": [round(full, 3)], "full_ms": round(full, 3),
-                      "efficiency": 1.0, "build_id": w.build_id(),
-                      "pool": os.environ.get("WGT_POOL", "0")}), flush=True)
+                      "efficiency": 1.0, "build_id": w.build_id()}), flush=True)
     for n in a.ns:
         ms = [timed(wd.shard_tiles(W, H, T, [(0, 0)], r, n)) for r in range(n)]
         print(json.dumps({"scene": a.scene, "n": n, "rank_ms": [round(x, 3) for x in ms], "full_ms": round(full, 3),
                           "max_rank_ms": round(max(ms), 3), "efficiency": round(full / (n * max(ms)), 4),
-                          "build_id": w.build_id(), "pool": os.environ.get("WGT_POOL", "0")}), flush=True)
+                          "build_id": w.build_id()}), flush=True)
     ctx.close()
 
 

@@ -43,6 +43,55 @@ def test_shards_cover_every_tile_once(wgt, world):
     assert wd.max_tiles_per_rank(W, H, T, world, world) == max(per_rank)
 
 
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_curve_dealing_gives_each_rank_one_tile_per_run(wgt, world):
+    """Every run of `world` consecutive Morton-curve positions holds one tile of each rank (in every
+    frame of the batch), so neighbouring tiles, whose costs are alike, spread over the ranks."""
+    from webgputracer_amd import dist as wd
+
+    W, H, T = 1920, 1080, 32
+    pos = wd.curve_positions(W, H, T)
+    assert sorted(pos.tolist()) == list(range(len(pos)))
+    xy = wd.frame_tiles(W, H, T)
+    for j in range(2):
+        owner = np.empty(len(pos), np.int64)
+        for r in range(world):
+            t = wd.shard_tiles(W, H, T, [(j, j)] * 1, r, world)
+            idx = [int(np.nonzero((xy[:, 0] == x) & (xy[:, 1] == y))[0][0]) for x, y in zip(t["x0"], t["y0"])]
+            owner[pos[idx]] = r
+        full = len(pos) // world * world  # (the last, partial run: at most one tile per rank)
+        runs = owner[:full].reshape(-1, world)
+        assert all(sorted(run.tolist()) == list(range(world)) for run in runs)
+
+
+@pytest.mark.parametrize("world", [3, 4, 8])
+@pytest.mark.parametrize("field", ["arcades4", "arcades8", "bands", "iid"])
+def test_curve_dealing_balances_a_structured_cost_field(wgt, field, world):
+    """Tile cost fields at 1080p in 32x32 tiles: expensive tile columns every 4 or 8 (arcades; row-
+    major dealing, t % N with 60 tiles per row, gives such a column to one rank), smooth bands with
+    a bright centre, and independent lognormal tile costs.  The curve dealing keeps every rank's
+    summed cost within 3% of the mean where costs repeat or vary smoothly, and within 8% for
+    independent costs (the spread of a sum of ~2040/N random tiles)."""
+    from webgputracer_amd import dist as wd
+
+    W, H, T = 1920, 1080, 32
+    xy = wd.frame_tiles(W, H, T)
+    col, row = xy[:, 0] // T, xy[:, 1] // T
+    cx, cy = xy[:, 0] / W, xy[:, 1] / H
+    if field.startswith("arcades"):
+        cost = 1.0 + 2.0 * (col % int(field[-1]) == 0) + 0.5 * (row % 2)
+    elif field == "bands":
+        cost = 1.0 + 0.8 * (np.sin(cx * 2 * np.pi * 3.3) > 0) + 2.0 * np.exp(-((cx - 0.5) ** 2 + (cy - 0.5) ** 2) * 8)
+    else:
+        cost = np.random.default_rng(0).lognormal(0.0, 0.5, len(xy))
+    ranks = wd.tile_ranks(W, H, T, 0, world)
+    per_rank = np.array([cost[ranks == r].sum() for r in range(world)])
+    assert per_rank.max() / per_rank.mean() < (1.08 if field == "iid" else 1.03)
+    if field == "arcades4" and world in (4, 8):
+        rowmajor = np.array([cost[np.arange(len(cost)) % world == r].sum() for r in range(world)])
+        assert rowmajor.max() / rowmajor.mean() > 1.2
+
+
 def test_assemble_single_rank(wgt):
     from webgputracer_amd import dist as wd
 

@@ -136,6 +136,7 @@ struct DevFrame {
   uint32_t n_slots, pq_refill, pq_lpt;
   uint32_t pq_lpt_all;  // the pre-pass renders all 64 pixels of each block (else the 16 at even x, y)
   uint32_t pq_svc_cost;  // pre-pass work units per ray started (a service iteration ~ 7 traversal steps)
+  uint32_t pq_depth;     // the pre-pass's paths end at this depth (kRayDepth: the full path)
   const uint32_t* perm;
   uint32_t* cost;
   // parked k_render_ps (DevScene::ps_park): the global part of the lanes' stacks, entry e

@@ -261,7 +261,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           const uint64_t ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
           const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
           ++depth;
-          if (end || depth == kRayDepth) {
+          // COST: the pre-pass's paths may end early (DevFrame::pq_depth): a cost estimate
+          if (end || depth == (COST ? (int)fr.pq_depth : kRayDepth)) {
             end_sample(fr, px, pc);
             depth = 0;
           }

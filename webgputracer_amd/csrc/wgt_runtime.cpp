@@ -225,6 +225,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   fr.pq_svc_cost = env_u32("WGT_PQ_SVC_COST", 7);
+  fr.pq_depth = env_u32("WGT_PQ_DEPTH", kRayDepth);
   fr.pq_lpt_all = env_u32("WGT_PQ_LPT_ALL", 1);  // sweep: all pixels -3% (sponza), -4% (bunny) at 256 spp
   return fr;
 }
@@ -412,8 +413,10 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
   if (timing) WGT_HIP(ctx, hipEventRecord(e0, s));
   int rc;
   // the next workspace slot: a launch on any stream first waits for the previous
-  // launch that used it (WGT_WS_SLOTS = 1 serialises every launch of the context)
-  const uint32_t n_slots = std::min<uint32_t>(std::max<uint32_t>(env_u32("WGT_WS_SLOTS", 2), 1u),
+  // launch that used it (WGT_WS_SLOTS = 1 serialises every launch of the context; 4 by
+  // default, one per pipeline stream, so that up to 4 frames are in flight: a strongly scaled
+  // rank's share of a frame holds fewer pixels than the device has lanes)
+  const uint32_t n_slots = std::min<uint32_t>(std::max<uint32_t>(env_u32("WGT_WS_SLOTS", wgt_ctx::kMaxWsSlots), 1u),
                                               (uint32_t)wgt_ctx::kMaxWsSlots);
   wgt_ctx::WsSlot& sl = ctx->slots[ctx->next_slot % n_slots];
   ctx->next_slot = (ctx->next_slot + 1) % n_slots;

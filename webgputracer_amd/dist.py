@@ -7,8 +7,13 @@ batch of frames, and rank 0 gathers the tiles and assembles the frames:
 
   * pixel (x, y) of frame f depends only on (x, y, W, H, seed_f, scene)
     (path_tracer.wgsl:378), so ANY partition reproduces the single-GPU frame bit
-    for bit; tiles are dealt round-robin (tile t of frame j -> rank (t + j) % N)
-    so the expensive and the cheap (escaping, NaN-absorbed) regions spread evenly;
+    for bit; tiles are dealt along a Morton (Z-order) curve over the tile grid: each
+    run of N consecutive curve positions (neighbouring tiles, whose costs are alike)
+    gives every rank one tile, the ranks rotated per run so that over N runs every
+    rank takes every place in a run once, in a hashed order that no lattice of the
+    tile grid lines up with; the expensive and the cheap (escaping, NaN-absorbed)
+    regions spread evenly (row-major dealing, t % N, left ranks 19% apart at N = 8
+    on the sponza frame, DESIGN.md §7);
   * weak scaling: a step renders N frames on N GPUs, i.e. one frame's worth of
     tiles per GPU; the only collective is one gather per step
     (torch.distributed backend "nccl" = RCCL on ROCm; "gloo" in CPU tests).
@@ -26,13 +31,58 @@ def frame_tiles(W: int, H: int, T: int):
     return np.stack([xs.ravel(), ys.ravel()], axis=1)
 
 
+def curve_positions(W: int, H: int, T: int):
+    """Position of every tile of frame_tiles(W, H, T) along the Morton curve over the tile grid
+    (ties impossible: distinct tiles have distinct codes)."""
+    xy = frame_tiles(W, H, T) // T
+    code = np.zeros(len(xy), np.uint64)
+    for b in range(16):  # interleave the bits of the tile column (even) and row (odd)
+        code |= ((xy[:, 0].astype(np.uint64) >> b) & 1) << (2 * b)
+        code |= ((xy[:, 1].astype(np.uint64) >> b) & 1) << (2 * b + 1)
+    pos = np.empty(len(xy), np.int64)
+    pos[np.argsort(code, kind="stable")] = np.arange(len(xy))
+    return pos
+
+
+def _hash32(x):
+    """The murmur3 32-bit finaliser, elementwise."""
+    h = np.asarray(x, np.uint64) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    h = (h * np.uint64(0x85EBCA6B)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(13)
+    h = (h * np.uint64(0xC2B2AE35)) & np.uint64(0xFFFFFFFF)
+    h ^= h >> np.uint64(16)
+    return h
+
+
+def run_rotations(n_runs: int, world: int):
+    """Rotation of the ranks for each run of `world` curve positions: the runs of each group of
+    `world` consecutive runs take the rotations 0 .. world-1 once each, in an order hashed from the
+    run index, so over a group every rank takes every place in a run once (no place's cost stays
+    with one rank) and no lattice of the tile grid lines up with the order."""
+    g = np.arange(n_runs, dtype=np.int64)
+    order = np.lexsort((_hash32(g), g // world))  # by group, then by hash within the group
+    rot = np.empty(n_runs, np.int64)
+    rot[order] = np.arange(n_runs) % world  # groups are contiguous in `order`, each of size world
+    # (the last group may be partial: its runs still take distinct rotations)
+    return rot
+
+
+def tile_ranks(W: int, H: int, T: int, j: int, world: int):
+    """Rank of every tile of frame_tiles(W, H, T) in the j-th frame of a batch: the tile at curve
+    position p (run p // world) goes to rank (p + j + run_rotations(...)[p // world]) % world."""
+    pos = curve_positions(W, H, T)
+    rot = run_rotations(int(pos.max()) // world + 1 if len(pos) else 0, world)
+    return (pos + j + rot[pos // world]) % world
+
+
 def shard_tiles(W: int, H: int, T: int, frames, rank: int, world: int):
-    """Tile list (TILE_DTYPE) of `rank` for the batch `frames` (list of (frame_id, seed)).
-    Tile t of the j-th frame of the batch goes to rank (t + j) % world."""
+    """Tile list (TILE_DTYPE) of `rank` for the batch `frames` (list of (frame_id, seed)), in
+    row-major tile order, dealt by tile_ranks."""
     xy = frame_tiles(W, H, T)
     out = []
     for j, (fid, seed) in enumerate(frames):
-        sel = np.nonzero((np.arange(len(xy)) + j) % world == rank)[0]
+        sel = np.nonzero(tile_ranks(W, H, T, j, world) == rank)[0]
         t = np.zeros(len(sel), TILE_DTYPE)
         t["x0"] = xy[sel, 0]
         t["y0"] = xy[sel, 1]
