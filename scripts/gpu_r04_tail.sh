@@ -16,4 +16,4 @@ for r in 1 2; do for d in 50 8 3; do
   WGT_PQ_DEPTH=$d timeout -k 10 600 python bench.py --scene sponza --steps 20 --warmup 5 --pmc off --no-cpu-baseline --stats-reps 1 > $O/bench_d${d}_$r.log 2>&1 || { tail -20 $O/bench_d${d}_$r.log; exit 1; }
   echo "pq_depth $d r$r: $(tail -1 $O/bench_d${d}_$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['kernel_ms'], d['timing']['isolated_launch_ms'])")"
 done; done
-bash scripts/gpu_r04_qmix.sh ${1:-r04tail}_qm
+[ -f ab/qaxis.so ] && bash scripts/gpu_r04_qmix.sh ${1:-r04tail}_qm
