@@ -225,7 +225,10 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
   fr.pq_svc_cost = env_u32("WGT_PQ_SVC_COST", 7);
-  fr.pq_depth = env_u32("WGT_PQ_DEPTH", kRayDepth);
+  // the pre-pass's paths end at depth 6 (a cost estimate needs the path's first bounces, and
+  // the full 50-bounce tail set the pre-pass's own drain): sponza +0.4%, bunny +0.7%, the frame
+  // alone -0.6% against full paths, 3 rounds on one box (profiles/sweeps/r04_pq_depth.log)
+  fr.pq_depth = std::min<uint32_t>(std::max<uint32_t>(env_u32("WGT_PQ_DEPTH", 6), 1u), (uint32_t)kRayDepth);
   fr.pq_lpt_all = env_u32("WGT_PQ_LPT_ALL", 1);  // sweep: all pixels -3% (sponza), -4% (bunny) at 256 spp
   return fr;
 }
