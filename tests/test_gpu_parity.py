@@ -335,6 +335,8 @@ _SCHED_REF = {}
                                  {"WGT_PQ_REFILL": "64"}, {"WGT_PS_TO_TRAV": "1", "WGT_PS_TO_SERVICE": "63"},
                                  {"WGT_PQ_LPT": "2"}, {"WGT_PQ_LPT_ALL": "0"}, {"WGT_PS_SVC_FRAC": "0"},
                                  {"WGT_PS_SVC_FRAC": "1"},
+                                 # the cost pre-pass's path depth (default 6): its shortest and the full path
+                                 {"WGT_PQ_DEPTH": "1"}, {"WGT_PQ_DEPTH": "50"},
                                  {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
                                  {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}, {"WGT_NARROW": "1"},
                                  {"WGT_STACK_LIMIT": "20"},
