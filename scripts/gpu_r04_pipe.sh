@@ -13,3 +13,8 @@ for r in $(seq $R); do
     echo "pipeline $p r$r: $(tail -1 $O/bench_p${p}_$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['kernel_ms'], d['timing']['isolated_launch_ms'])")"
   done
 done
+# the driver's exact command three times back to back (repeatability of the line on this build)
+for r in 1 2 3; do
+  timeout -k 10 600 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > $O/bench20_run$r.log 2>&1 || { tail -20 $O/bench20_run$r.log; exit 1; }
+  echo "driver command run $r: $(tail -1 $O/bench20_run$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['roofline']['frac'], d['roofline'].get('traffic_source'))")"
+done
