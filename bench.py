@@ -5,7 +5,7 @@ on, and the one north_star's roofline target names): Sponza-sized procedural sta
 (268,944 triangles; the asset is absent and there is no network) inside the reference
 Cornell box + light, 1920x1080, 256 spp.  `--scene bunny` runs configs[2] (C3).  A
 "step" renders one 1080p/256spp frame per GPU: the step's N frames are cut into 32x32
-tiles dealt round-robin over the N ranks (one process per GPU), then the tiles are
+tiles dealt over the N ranks along a Morton curve (one process per GPU), then the tiles are
 gathered to rank 0 (RCCL over xGMI) and assembled — weak scaling, per-GPU work fixed.
 Steps are issued two deep (--pipeline 2): step k runs on the context's pipeline stream
 k % 2 into output set k % 2, so each frame starts in the previous frame's end-of-launch

@@ -159,7 +159,7 @@ def gather_tiles(local, rank: int, world: int, dist, dst: int = 0):
 
 class ShardedFrames:
     """One rank's share of a step (bench.py's N>1 path, and its GPU test): the
-    step's frames cut into T x T tiles dealt round-robin (shard_tiles), one
+    step's frames cut into T x T tiles dealt along the Morton curve (shard_tiles), one
     tile-list launch into a compact device buffer (wgt_render_tiles_async), one
     gather to rank 0 (RCCL over xGMI with backend "nccl"; gloo gathers host
     copies) and rank 0's assembly with a single index op built once here.
