@@ -45,6 +45,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # (the padded box with the Moller-Trumbore inputs), a traced
 # ray 32 B of per-triangle shading data
 NODE_BYTES, CNODE_BYTES, C64NODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 64, 64, 32
+W8NODE_BYTES = 128  # a wide 8-slot record (round 5): one whole 128-B line per visit
 # SURVEY §8(d)'s format-independent figure: 32 B per BVH node visit, 48 B per triangle
 # test, 32 B of shading record per traced ray (the same at any node encoding)
 SURVEY_NODE_BYTES, SURVEY_TRI_BYTES = 32, 48
@@ -54,7 +55,7 @@ L2_CALIB_JSON = os.path.join(ROOT, "profiles", "l2_calibration.json")
 
 def dominant_kernel(form: int, waves: int, tris: bool = True, park: bool = True) -> str:
     """The timed k_render_ps instantiation <STATS, COST, node form (0 = 128-B, 1 = 80-B compact,
-    2 = 64-B compact), waves per SIMD, triangles, parked traversal state> (a scene without
+    2 = 64-B compact, 3 = wide), waves per SIMD, triangles, parked traversal state> (a scene without
     triangles runs the 8-wave instantiation without traversal)."""
     if not tris:
         return "wgt::k_render_ps<false, false, 0, 8, false, false>"
@@ -62,9 +63,13 @@ def dominant_kernel(form: int, waves: int, tris: bool = True, park: bool = True)
 
 
 def node_form(info) -> int:
-    """The node form k_render_ps reads (wgt_kernels.hip node_form; WGT_CNODE: 0 = 128-B, 1 = 80-B
-    compact, 2 = 80-B compact when the 128-B tree exceeds 4 MB (default), 3 = 64-B compact where the
-    tree fits it (scene_info bvh_c64), else 80-B): 0 = 128-B, 1 = 80-B, 2 = 64-B."""
+    """The node form k_render_ps reads (wgt_kernels.hip node_form): 0 = 128-B, 1 = 80-B compact,
+    2 = 64-B compact, 3 = wide 8-slot records.  The library reports it for the reference camera
+    (scene_info node_form, round 5); an older build (A/B runs) is mirrored from WGT_CNODE: 0 = 128-B,
+    1 = 80-B compact, 2 = 80-B compact when the 128-B tree exceeds 4 MB, 3 = 64-B compact where the
+    tree fits it (scene_info bvh_c64), else 80-B."""
+    if "node_form" in info and info.get("bvh_w8", 0) in (0, 1) and info["node_form"] in (0, 1, 2, 3):
+        return int(info["node_form"])
     mode = os.environ.get("WGT_CNODE", "2") or "2"
     if mode == "3":
         return 2 if info.get("bvh_c64", 0) and info.get("ps_waves") == 6 else 1
@@ -306,8 +311,11 @@ def main():
     cam = w.camera_param(W / H, spp, 0)  # per-tile seeds override cam.seed
     # the rank's tiles, its compact output buffer and (rank 0) the assembly index, all resident
     P = max(1, min(args.pipeline, 4))
+    # output sets: twice the frames in flight, so that a set's gather (on the shard's gather stream,
+    # decoupled from the render streams) has a whole step to finish before the set is written again
+    D = 2 * P
     shard = wdist.ShardedFrames(ctx, cam, W, H, T, frames, rank, world, dist, dev, backend=args.dist_backend,
-                                depth=P)
+                                depth=D)
 
     # instrumented passes (untimed): exact ray/sample counts for this rank's tiles.  The
     # node / triangle counts depend slightly on the schedule (which lanes run the
@@ -325,16 +333,20 @@ def main():
     torch.cuda.set_stream(streams[0])
 
     def step(k, ev):
-        s = streams[k % P]
+        # step k: render on stream k % P into output set k % D (after the gather that last read the
+        # set), then gather + assemble on the gather stream, which no render launch waits for: a
+        # launch never queues behind a collective whose kernels wait for CUs
+        s, slot = streams[k % P], k % D
         with torch.cuda.stream(s):
+            shard.wait_slot(s, slot)
             if ev is not None:
                 ev[0].record(s)
-            shard.launch(s.cuda_stream, slot=k % P)
+            shard.launch(s.cuda_stream, slot=slot)
             if ev is not None:
                 ev[1].record(s)
-            got = shard.gather(slot=k % P)
-            if ev is not None:
-                ev[2].record(s)
+        got = shard.gather_async(slot, s)
+        if ev is not None:
+            ev[2].record(shard.gather_stream)
         return got["u8"] if got is not None else None
 
     for k in range(args.warmup):
@@ -382,6 +394,7 @@ def main():
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         with torch.cuda.stream(streams[0]):
+            shard.wait_slot(streams[0], 0)
             e0.record(streams[0])
             shard.launch(streams[0].cuda_stream, slot=0)
             e1.record(streams[0])
@@ -411,7 +424,7 @@ def main():
         form = node_form(info)
         kernel = dominant_kernel(form, int(info.get("ps_waves", 5)), info["n_tris"] > 0,
                                  bool(info.get("ps_park", 0)))
-        node_b = (NODE_BYTES, CNODE_BYTES, C64NODE_BYTES)[form]
+        node_b = (NODE_BYTES, CNODE_BYTES, C64NODE_BYTES, W8NODE_BYTES)[form]
         bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         survey_bytes = mine[4] * SURVEY_NODE_BYTES + mine[5] * SURVEY_TRI_BYTES + mine[1] * SHADE_BYTES
@@ -486,7 +499,8 @@ def main():
             "config": {"workload": f"{args.scene}-{W}x{H}-{spp}spp", "width": W, "height": H, "spp": spp,
                        "triangles": n_tris, "bvh_nodes": info["bvh_nodes"], "tile": T,
                        "frames_per_step": len(frames),
-                       "parallelism": f"tiles{world}+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}-gather"},
+                       "parallelism": "1 GPU, no collective" if world == 1 else
+                       f"tiles{world}+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}-gather"},
             "samples_per_s": round(samples / max_t, 1),
             "reference_queries_per_s": round(queries / max_t, 1),
             "kernel_ms": round(kern_ms, 3),
@@ -499,7 +513,8 @@ def main():
             "simt_utilisation": {k: round(v, 4) for k, v in simt.items()},
             "per_launch": {"traced_rays": int(mine[1]), "node_visits": int(mine[4]), "tri_tests": int(mine[5]),
                            "algorithmic_bytes": int(survey_bytes), "loaded_bytes": int(bytes_launch),
-                           "kernel": kernel, "bvh_nodes": ("128 B", "compact 80-B records", "compact 64-B records")[form]},
+                           "kernel": kernel, "bvh_nodes": ("128 B", "compact 80-B records", "compact 64-B records",
+                                                                     "wide 8-slot 128-B records")[form]},
             # achieved = SURVEY 8(d)'s algorithmic bytes (32 B per node visit, 48 B per triangle test, 32 B
             # per traced ray: independent of the node encoding) / the launch time.  The roofline priced is
             # HBM's; `bound` is what the measurements show bounds the kernel (limiter())

@@ -244,18 +244,24 @@ def test_bunny_1080p_256spp_subsample(ctx, wgt, oracle, bunny):
 _SPONZA = {}
 
 
-@pytest.mark.parametrize("cnode", ["2", "0", "3"])
-def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
-    """Sponza stand-in: by default (2) the persistent kernel reads the 80-B compact records
-    (the 128-B tree exceeds one XCD's L2), 0 forces the 128-B nodes, 3 the 64-B compact
-    records."""
-    monkeypatch.setenv("WGT_CNODE", cnode)
+def _sponza(wgt, oracle):
+    """The sponza stand-in and the oracle's 80x45 / 4 spp render of it (built once)."""
     if not _SPONZA:
         L, Q, S, T = wgt.mesh_scene("sponza")
         osc = oracle.OracleScene(L, Q, S, T)
         _SPONZA["scene"] = (L, Q, S, T)
         _SPONZA["r"] = osc.render(oracle.camera_param(16 / 9, 4, 5), 80, 45)
-    L, Q, S, T = _SPONZA["scene"]
+        osc.close()
+    return _SPONZA["scene"]
+
+
+@pytest.mark.parametrize("cnode", ["2", "0", "3", "4"])
+def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
+    """Sponza stand-in: by default (2) the persistent kernel reads the 80-B compact records
+    (the 128-B tree exceeds one XCD's L2), 0 forces the 128-B nodes, 3 the 64-B compact
+    records, 4 the wide 8-slot records."""
+    monkeypatch.setenv("WGT_CNODE", cnode)
+    L, Q, S, T = _sponza(wgt, oracle)
     ctx.upload_scene(L, Q, S, T)
     g = ctx.render_tile(wgt.camera_param(16 / 9, 4, 5), 80, 45, stats=True)
     r = _SPONZA["r"]
@@ -264,7 +270,8 @@ def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
     check_counters(g["stats"], r["counters"], oracle)
     info = ctx.scene_info()
     assert info["n_tris"] == len(T) and info["bvh_max_depth"] <= 94
-    assert info["bvh_compact"] == 1 and info["bvh_c64"] == 1
+    assert info["bvh_compact"] == 1 and info["bvh_c64"] == 1 and info["bvh_w8"] == 1
+    assert info["node_form"] == {"2": 1, "0": 0, "3": 2, "4": 3}[cnode]
 
 
 _FULL = {}
@@ -272,7 +279,8 @@ _FULL = {}
 
 @pytest.mark.parametrize("kind,spp,env", [("sponza", 4, {}), ("sponza", 4, {"WGT_CNODE": "3"}),
                                           ("sponza", 4, {"WGT_PARK": "1"}), ("sponza", 4, {"WGT_PS_WAVES": "7"}),
-                                          ("bunny", 1, {})])
+                                          ("sponza", 4, {"WGT_CNODE": "4"}), ("bunny", 1, {}),
+                                          ("bunny", 1, {"WGT_CNODE": "4"})])
 def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatch):
     """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
     oracle (OpenMP), through the default kernel of each scene: sponza on the 80-B compact
@@ -301,9 +309,7 @@ def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatc
 def test_sponza_1080p_256spp_subsample_compact(ctx, wgt, oracle):
     """BASELINE config 4 (the bench workload) at full size through the compact nodes:
     GPU tiles of the 1920x1080/256spp frame vs the oracle on the same global pixels."""
-    if not _SPONZA:
-        pytest.skip("needs test_sponza_render_parity's scene")
-    L, Q, S, T = _SPONZA["scene"]
+    L, Q, S, T = _sponza(wgt, oracle)
     ctx.upload_scene(L, Q, S, T)
     osc = oracle.OracleScene(L, Q, S, T)
     cam_g, cam_o = wgt.camera_param(16 / 9, 256, 0), oracle.camera_param(16 / 9, 256, 0)
@@ -352,6 +358,14 @@ _SCHED_REF = {}
                                  # 7 waves per SIMD (parked state only)
                                  {"WGT_PS_WAVES": "7"}, {"WGT_PS_WAVES": "7", "WGT_CNODE": "1"},
                                  {"WGT_PS_WAVES": "7", "WGT_CNODE": "3", "WGT_PS_CAP": "8"},
+                                 # the wide 8-slot records (round 5): 3-byte and (5 waves) 4-byte group
+                                 # entries, block order, every lane in every traversal phase, triangle
+                                 # steps as soon as one lane has a group open (1) or node steps while any
+                                 # lane has a node (the most second triangle groups pushed)
+                                 {"WGT_CNODE": "4"}, {"WGT_CNODE": "4", "WGT_PQ_LPT": "0"},
+                                 {"WGT_CNODE": "4", "WGT_PS_WAVES": "5"},
+                                 {"WGT_CNODE": "4", "WGT_PS_TO_TRAV": "1", "WGT_PS_TO_SERVICE": "63"},
+                                 {"WGT_CNODE": "4", "WGT_TRI_RATIO": "1"}, {"WGT_CNODE": "4", "WGT_TRI_RATIO": "1000000"},
                                  ])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the

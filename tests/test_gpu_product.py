@@ -356,6 +356,59 @@ dist.destroy_process_group()
 """
 
 
+_RCCL_PIPELINE = r"""
+import os, sys, json
+import numpy as np, torch, torch.distributed as dist
+sys.path.insert(0, os.environ["WGT_ROOT"])
+import webgputracer_amd as w
+from webgputracer_amd import dist as wdist
+dev = torch.device("cuda", 0)
+torch.cuda.set_device(dev)
+dist.init_process_group("nccl", device_id=dev)  # RCCL on ROCm
+ctx = w.Context(0)
+ctx.upload_scene(*w.mesh_scene("bunny", target_tris=2000))
+W, H, T, P, D = 160, 96, 32, 2, 4
+cam = w.camera_param(W / H, 4, 0)
+frames = [(7, 11), (8, 12)]
+# bench.py's step loop: launches on the context's two pipeline streams into output set k % D, each
+# set's gather + assembly on the gather stream through the process group's gather (collective=True:
+# RCCL with one rank), waited for only by the launch that next writes the set
+sh = wdist.ShardedFrames(ctx, cam, W, H, T, frames, 0, 1, dist, dev, backend="nccl", depth=D, collective=True)
+streams = [torch.cuda.ExternalStream(ctx.pipeline_stream(i), device=dev) for i in range(P)]
+outs = []
+for k in range(9):
+    s, slot = streams[k % P], k % D
+    with torch.cuda.stream(s):
+        sh.wait_slot(s, slot)
+        sh.launch(s.cuda_stream, slot=slot)
+    got = sh.gather_async(slot, s)
+    outs.append(got["u8"])
+torch.cuda.synchronize()
+refs = ctx.render_frames(cam, W, H, np.array([sd for _, sd in frames], np.uint32))
+ok = all(np.array_equal(o[fid].cpu().numpy(), refs[i]) for o in outs for i, (fid, _) in enumerate(frames))
+print(json.dumps({"backend": dist.get_backend(), "steps": len(outs), "frames_equal": bool(ok)}))
+ctx.close()
+dist.destroy_process_group()
+"""
+
+
+def test_rccl_pipelined_gather_one_rank(tmp_path):
+    """bench.py's N > 1 step loop at one rank through the real RCCL gather (not the one-rank
+    short cut): launches alternate over two pipeline streams into four output sets, each set's
+    gather and assembly run on the shard's gather stream, and a launch waits only for the gather
+    that last read its set (dist.ShardedFrames.wait_slot / gather_async).  Every gathered frame of
+    9 steps equals the single-launch render of its seed."""
+    import json
+
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(_free_port()), WGT_ROOT=ROOT)
+    r = subprocess.run([sys.executable, "-c", _RCCL_PIPELINE], capture_output=True, text=True, timeout=240,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line == {"backend": "nccl", "steps": 9, "frames_equal": True}, line
+
+
 def test_rccl_backend_one_rank(tmp_path):
     """The RCCL ("nccl") backend initialises and runs bench.py's two collectives (the tile gather
     to rank 0 and the all_gather of the timing vector) on this box's GPU, with one rank (RCCL

@@ -54,7 +54,11 @@ class WgtSceneInfo(ctypes.Structure):
                 ("device_bytes", ctypes.c_uint64), ("sah_cost", ctypes.c_double), ("bvh_width", ctypes.c_uint32),
                 ("bvh_stack", ctypes.c_uint32), ("bvh2_nodes", ctypes.c_uint32), ("bvh2_depth", ctypes.c_uint32),
                 ("bvh_compact", ctypes.c_uint32), ("bvh_compact_step", ctypes.c_float), ("ps_waves", ctypes.c_uint32),
-                ("ps_park", ctypes.c_uint32), ("ps_stack", ctypes.c_uint32), ("bvh_c64", ctypes.c_uint32)]
+                ("ps_park", ctypes.c_uint32), ("ps_stack", ctypes.c_uint32), ("bvh_c64", ctypes.c_uint32),
+                ("bvh_w8", ctypes.c_uint32), ("w8_groups", ctypes.c_uint32), ("w8_nodes", ctypes.c_uint32),
+                ("w8_leaves", ctypes.c_uint32), ("w8_depth", ctypes.c_uint32), ("w8_stack", ctypes.c_uint32),
+                ("w8_step", ctypes.c_float), ("w8_sah", ctypes.c_double), ("w8_records", ctypes.c_uint32),
+                ("w8_bound", ctypes.c_float), ("node_form", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -67,7 +71,8 @@ EXPORTS = [
     "wgt_render_tiles_stats", "wgt_render_tiles_profile", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_selftest_math", "wgt_stream",
     "wgt_pipeline_stream",
     "wgt_scene_cornell", "wgt_make_triangles", "wgt_load_obj", "wgt_procedural_mesh",
-    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build", "wgt_bvh_build_compact", "wgt_render_frames",
+    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build", "wgt_bvh_build_compact", "wgt_bvh_build_wide",
+    "wgt_render_frames",
 ]
 
 _lib = None
@@ -123,6 +128,7 @@ def lib():
         "wgt_write_obj": (I, [ctypes.c_char_p, P, U32]),
         "wgt_write_png": (I, [ctypes.c_char_p, P, U32, U32]),
         "wgt_bvh_build": (I, [P, U32, P, U32, P, ctypes.POINTER(WgtSceneInfo)]),
+        "wgt_bvh_build_wide": (I, [P, U32, P, U32, P, U32, ctypes.POINTER(WgtSceneInfo)]),
         "wgt_render_frames": (I, [P, P, U32, U32, P, U32, P, P]),
     }
     for name, (res, args) in sig.items():

@@ -25,6 +25,15 @@ struct BvhOut {
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;  // BVH4 nodes / depth
   uint32_t n_nodes2 = 0, depth2 = 0;  // the SAH BVH2 the BVH4 was collapsed from
   uint32_t stack_need = 0;            // worst-case traversal stack entries (exact for this tree)
+  // the wide form (wgt_geom.h kW8*): records 8g + s of 32 words, triangle records 4(8g + s) + i
+  // of kTriRecordFloats, over its own BVH2 (leaves <= kW8LeafMax); w8_ok = false without it
+  bool w8_ok = false;
+  std::vector<uint32_t> w8nodes;
+  std::vector<float> w8tris;
+  std::vector<uint32_t> w8leaf;  // per group: the L word of the record that owns it
+  uint32_t w8_groups = 0, w8_nodes = 0, w8_leaves = 0, w8_depth = 0, w8_stack = 0;
+  float w8step = 1.0f;
+  double w8_sah = 0.0;
   bool narrow = false;                // collapsed under narrow_limit (BuildBvh)
   double sah_cost = 0.0;
 };

@@ -51,6 +51,13 @@ struct DevScene {
   // 1 / step; c64bound < 0 when the tree's refs or origins do not fit the form
   const float4* __restrict__ cnodes64;
   float c64step, rc64step, c64bound;
+  // the wide form (wgt_geom.h kW8*): 128-B records and its own triangle records, their decode
+  // step and 1 / step (the same origin bound cbound); w8 = 0 when the tree has no wide form
+  const float4* __restrict__ w8nodes;
+  const float4* __restrict__ w8tris;
+  const uint32_t* __restrict__ w8leaf;  // per group g: its records' L word (a popped triangle group's mask)
+  float w8step, rw8step;
+  uint32_t w8;
   uint32_t n_lights, n_quads, n_spheres, n_tris;
   uint32_t n_nodes;
   uint32_t last_sphere_emissive;

@@ -123,6 +123,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   extern __shared__ int s_stack[];  // stack entries per lane (+ parked words), ps_stack_lds_bytes
   // 6 or 7 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
   using STK = typename std::conditional<W >= 6, Stack24, Stack32>::type;
+  static_assert(!(PK && CN == 3), "the wide form keeps its whole stack in LDS");
   const uint32_t cap = PK ? sc.ps_cap : sc.stack;  // LDS stack entries per lane
   // PK: the highest stack top a node step may start from, cap - 4 (3 pushes and a parked
   // leaf above it); no bound when the LDS holds the builder's whole stack (cap = sc.stack),
@@ -307,7 +308,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             }
             // (PK: a root step pushes at most 4 entries, and the LDS stack holds >= kMinPsCap
             // = 8, so the ray starts its traversal with a top <= top_max)
-            if (trav_done(t)) pending = true;
+            if (trav_fin<CN>(t)) pending = true;
             else trav = true;
           } else {
             pending = true;  // no triangles: the quad and sphere scans are the whole query
@@ -339,17 +340,21 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       // one uniform mode per step: triangle steps once enough lanes hold a
       // pending leaf (weighted by the two steps' costs), else node steps
       const bool can_node = t.ref != kNoRef;  // implies trav (invariant above)
-      const bool can_tri = t.lf < t.le;       // implies trav
+      const bool can_tri = CN == 3 ? w8_can_tri(t) : t.lf < t.le;  // implies trav
       const uint32_t nn = (uint32_t)__popcll(__ballot(can_node));
       const uint32_t nl = (uint32_t)__popcll(__ballot(can_tri));
       const bool tri_mode = nn == 0 || nl * 100u >= nn * fr.tri_ratio;
       if (STATS && (tri_mode ? can_tri : can_node)) simt_count(st.wave_steps, st.lane_steps);
       if (COST && (tri_mode ? can_tri : can_node)) ++work;
       if (tri_mode) {
-        if (can_tri) tri_step<STATS, CN>(sc, ro, rd, t, lds, st);
+        if (can_tri) {
+          if constexpr (CN == 3) tri_step_w8<STATS>(sc, ro, rd, t, lds, st);
+          else tri_step<STATS, CN>(sc, ro, rd, t, lds, st);
+        }
       } else {
         if (can_node) {
-          node_step<STATS, CN>(sc, t, lds, st);
+          if constexpr (CN == 3) node_step_w8<STATS>(sc, t, lds, st);
+          else node_step<STATS, CN>(sc, t, lds, st);
           // PK: fewer than 4 free LDS entries above the top (only node steps push): the
           // lane parks its state and leaves as if done; its service pass spills (park_fix)
           if (PK && (uint32_t)t.sp > top_max) {
@@ -361,7 +366,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           }
         }
       }
-      if (trav && trav_done(t)) {
+      if (trav && trav_fin<CN>(t)) {
         trav = false;
         pending = true;
       }
@@ -511,7 +516,9 @@ template <bool STATS, bool COST, int CN, int W>
 void ps_launch_w(const DevScene& sc, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
                  const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
                  uint32_t* queue) {
-  if (sc.ps_park)
+  if constexpr (CN == 3)  // the wide form: the whole stack in LDS (node_form never picks it parked)
+    k_render_ps<STATS, COST, 3, W, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
+  else if (sc.ps_park)
     k_render_ps<STATS, COST, CN, W, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
   else
     k_render_ps<STATS, COST, CN, W, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
@@ -529,11 +536,13 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
     else if (cn == 1) k_render_ps<STATS, COST, 1, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
     else k_render_ps<STATS, COST, 0, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
   } else if (sc.ps_waves == 6) {
-    if (cn == 2) ps_launch_w<STATS, COST, 2, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    if (cn == 3) ps_launch_w<STATS, COST, 3, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    else if (cn == 2) ps_launch_w<STATS, COST, 2, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
     else if (cn == 1) ps_launch_w<STATS, COST, 1, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
     else ps_launch_w<STATS, COST, 0, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
   } else {
-    if (cn) ps_launch_w<STATS, COST, 1, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    if (cn == 3) ps_launch_w<STATS, COST, 3, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    else if (cn) ps_launch_w<STATS, COST, 1, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
     else ps_launch_w<STATS, COST, 0, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
   }
 }
@@ -544,8 +553,10 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
 // 4 MB L2 (sponza stand-in: 7.3 MB -> 4.6 MB; default), 3 = 64-B (at 6 waves per SIMD, when
 // the tree fits the form; else as 1).  A tree that fits keeps the 128-B nodes, whose step
 // needs fewer VALU.
+// 4 = the wide 8-slot records (when the scene has them and the traversal state is not parked).
 int node_form(const DevScene& sc, const DevFrame& fr) {
   const float cam = fmaxf(fmaxf(fabsf(fr.ox), fabsf(fr.oy)), fabsf(fr.oz));
+  if (fr.cnode == 4 && sc.w8 && !sc.ps_park && sc.ps_waves <= 6 && cam <= sc.cbound) return 3;
   if (fr.cnode == 3 && sc.ps_waves >= 6 && cam <= sc.c64bound) return 2;
   if (!(cam <= sc.cbound)) return 0;
   return fr.cnode == 1 || fr.cnode == 3 ||
@@ -633,40 +644,43 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   return hipGetLastError();
 }
 
+// k_render_ps<STATS = false, COST = false, CN, W> of a launchable form
 template <int W, bool PK>
-const void* ps_kernel(bool stats, bool cn) {
-  if (stats) return cn ? reinterpret_cast<const void*>(&k_render_ps<true, false, 1, W, true, PK>)
-                       : reinterpret_cast<const void*>(&k_render_ps<true, false, 0, W, true, PK>);
-  return cn ? reinterpret_cast<const void*>(&k_render_ps<false, false, 1, W, true, PK>)
-            : reinterpret_cast<const void*>(&k_render_ps<false, false, 0, W, true, PK>);
+const void* ps_kernel(int cn) {
+  if constexpr (W == 7) {
+    return cn == 2 ? reinterpret_cast<const void*>(&k_render_ps<false, false, 2, 7, true, true>)
+                   : cn == 1 ? reinterpret_cast<const void*>(&k_render_ps<false, false, 1, 7, true, true>)
+                             : reinterpret_cast<const void*>(&k_render_ps<false, false, 0, 7, true, true>);
+  } else {
+    if (cn == 3) return reinterpret_cast<const void*>(&k_render_ps<false, false, 3, W, true, false>);
+    if (cn == 2 && W == 6) return reinterpret_cast<const void*>(&k_render_ps<false, false, (W == 6 ? 2 : 1), W, true, PK>);
+    return cn ? reinterpret_cast<const void*>(&k_render_ps<false, false, 1, W, true, PK>)
+              : reinterpret_cast<const void*>(&k_render_ps<false, false, 0, W, true, PK>);
+  }
 }
 
+// The persistent grid: the smallest resident capacity over the node forms the scene's launches can
+// read (node_form), so that every wave of a launch is resident from its start.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
-  const void* notris[2] = {reinterpret_cast<const void*>(&k_render_ps<false, false, 0, kPsWavesNoTris, false>),
-                           reinterpret_cast<const void*>(&k_render_ps<true, false, 0, kPsWavesNoTris, false>)};
-  const void* variants[4];
-  for (int i = 0; i < 4; ++i) {
-    const bool stats = i & 1, cn = i >> 1;
-    if (sc.ps_waves == 7) variants[i] = ps_kernel<7, true>(stats, cn);
-    else if (sc.ps_waves == 6) variants[i] = sc.ps_park ? ps_kernel<6, true>(stats, cn) : ps_kernel<6, false>(stats, cn);
-    else variants[i] = sc.ps_park ? ps_kernel<5, true>(stats, cn) : ps_kernel<5, false>(stats, cn);
-  }
-  // the largest of the variants' capacities: waves beyond a variant's capacity
-  // start as others retire and find the queue drained or nearly so
   int per_cu = 0, cus = 0;
-  for (const void* k : variants) {
-    if (sc.n_tris == 0) break;
-    int n = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, ps_stack_lds_bytes(sc));
+  if (sc.n_tris == 0) {
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&k_render_ps<false, false, 0, kPsWavesNoTris, false>), kBlock,
+        stack_lds_bytes(sc));
     if (e != hipSuccess) return e;
-    per_cu = n > per_cu ? n : per_cu;
-  }
-  for (const void* k : notris) {
-    if (sc.n_tris != 0) break;
-    int n = 0;
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, stack_lds_bytes(sc));
-    if (e != hipSuccess) return e;
-    per_cu = n > per_cu ? n : per_cu;
+  } else {
+    per_cu = 1 << 30;
+    for (int cn = 0; cn < 4; ++cn) {
+      if (cn == 2 && !(sc.ps_waves >= 6 && sc.c64bound >= 0.0f)) continue;
+      if (cn == 3 && !(sc.w8 && !sc.ps_park && sc.ps_waves <= 6)) continue;
+      const void* k = sc.ps_waves == 7 ? ps_kernel<7, true>(cn)
+                      : sc.ps_waves == 6 ? (sc.ps_park ? ps_kernel<6, true>(cn) : ps_kernel<6, false>(cn))
+                                         : (sc.ps_park ? ps_kernel<5, true>(cn) : ps_kernel<5, false>(cn));
+      int n = 0;
+      const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, ps_stack_lds_bytes(sc));
+      if (e != hipSuccess) return e;
+      per_cu = n < per_cu ? n : per_cu;
+    }
   }
   const hipError_t e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device);
   if (e != hipSuccess) return e;

@@ -184,6 +184,18 @@ void ps_park_cap(uint32_t n_tris, uint32_t stack, uint32_t waves, uint32_t& park
   cap = std::max(c, kMinPsCap);
 }
 
+// The wide form's figures in wgt_scene_info (usable: the scene's launches can read it).
+void fill_w8_info(const BvhOut& bvh, bool usable, wgt_scene_info& in) {
+  in.bvh_w8 = usable ? 1u : 0u;
+  in.w8_groups = bvh.w8_groups;
+  in.w8_nodes = bvh.w8_nodes;
+  in.w8_leaves = bvh.w8_leaves;
+  in.w8_depth = bvh.w8_depth;
+  in.w8_stack = bvh.w8_stack;
+  in.w8_step = bvh.w8step;
+  in.w8_sah = bvh.w8_sah;
+}
+
 DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   DevFrame fr{};
   const float theta = radians_w(cam.fovy);
@@ -219,7 +231,8 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.ps_to_trav = env_u32("WGT_PS_TO_TRAV", 0);
   fr.ps_to_service = env_u32("WGT_PS_TO_SERVICE", 0);
   fr.ps_svc_frac = env_u32("WGT_PS_SVC_FRAC", 16);  // sweep: profiles/sweeps/r01_ps_svc_frac.jsonl
-  fr.tri_ratio = env_u32("WGT_TRI_RATIO", 100);
+  // >= 1: with 0 a wave whose lanes all hold a node but no open leaf would take triangle steps forever
+  fr.tri_ratio = std::max<uint32_t>(env_u32("WGT_TRI_RATIO", 100), 1u);
   fr.cnode = env_u32("WGT_CNODE", 2);  // compact nodes once the 128-B tree outgrows an XCD's L2
   fr.pq_refill = env_u32("WGT_PQ_REFILL", 0);  // 0 = the default, 2 (launch_render)
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
@@ -574,6 +587,34 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   info->bvh_c64 = c64_fits(bvh) ? 1u : 0u;
   ps_park_cap(n_tris, (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u, info->ps_waves, info->ps_park,
               info->ps_stack);
+  fill_w8_info(bvh, bvh.w8_ok, *info);
+  return WGT_OK;
+}
+
+int wgt_bvh_build_wide(const wgt_triangle* tris, uint32_t n_tris, uint32_t* recs_out, uint32_t recs_cap,
+                       float* tris_out, uint32_t tri_recs_cap, wgt_scene_info* info) {
+  if (!tris || n_tris == 0 || !info) return fail(nullptr, WGT_E_INVALID, "null triangles or info");
+  BvhOut bvh;
+  std::string err;
+  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(),
+                kOriginBoundScale * scene_extent(nullptr, 0, nullptr, 0, tris, n_tris), bvh, err))
+    return fail(nullptr, WGT_E_INVALID, err);
+  if (!bvh.w8_ok) return fail(nullptr, WGT_E_INVALID, "the tree has no wide form");
+  *info = wgt_scene_info{};
+  info->n_tris = n_tris;
+  info->bvh_compact_step = bvh.cstep;
+  fill_w8_info(bvh, true, *info);
+  info->w8_records = (uint32_t)(bvh.w8nodes.size() / kW8RecordWords);
+  info->w8_bound = bvh.cbound;
+  if (recs_out) {
+    if (recs_cap < info->w8_records) return fail(nullptr, WGT_E_INVALID, "record capacity too small");
+    std::memcpy(recs_out, bvh.w8nodes.data(), bvh.w8nodes.size() * 4);
+  }
+  if (tris_out) {
+    if ((size_t)tri_recs_cap * kTriRecordFloats < bvh.w8tris.size())
+      return fail(nullptr, WGT_E_INVALID, "triangle record capacity too small");
+    std::memcpy(tris_out, bvh.w8tris.data(), bvh.w8tris.size() * 4);
+  }
   return WGT_OK;
 }
 
@@ -675,7 +716,15 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const size_t b_tris = align256(dtris.size() * 4);
   const size_t b_shade = align256(bvh.tshade.size() * 4);
   const size_t b_c64 = align256(c64rec.size() * 4);
-  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64;
+  // the wide form (wgt_geom.h kW8*): its records and triangle records; Stack24 entries hold a
+  // 15-bit group index (6 waves per SIMD), Stack32 ones 23 bits
+  const uint32_t waves = ps_waves_for(bvh, n_tris);
+  const bool w8 = n_tris > 0 && bvh.w8_ok && bvh.w8_stack <= (uint32_t)kStackMax + 1u &&
+                  bvh.w8_groups < (waves >= 6 ? (1u << 15) : (1u << 23));
+  const size_t b_w8 = w8 ? align256(bvh.w8nodes.size() * 4) : 0;
+  const size_t b_w8t = w8 ? align256(bvh.w8tris.size() * 4) : 0;
+  const size_t b_w8l = w8 ? align256(bvh.w8leaf.size() * 4) : 0;
+  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64 + b_w8 + b_w8t + b_w8l;
 
   {
     int rc = use_drain(ctx);  // no launch on any stream may still read the old scene
@@ -710,6 +759,12 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     if (c64)
       std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes, c64rec.data(),
                   c64rec.size() * 4);
+    if (w8) {
+      char* w8base = host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64;
+      std::memcpy(w8base, bvh.w8nodes.data(), bvh.w8nodes.size() * 4);
+      std::memcpy(w8base + b_w8, bvh.w8tris.data(), bvh.w8tris.size() * 4);
+      std::memcpy(w8base + b_w8 + b_w8t, bvh.w8leaf.data(), bvh.w8leaf.size() * 4);
+    }
   }
   WGT_HIP(ctx, hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
 
@@ -722,6 +777,12 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.tshade = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris);
   sc.cnodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade);
   sc.cnodes64 = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes);
+  sc.w8nodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64);
+  sc.w8tris = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64 + b_w8);
+  sc.w8leaf = (const uint32_t*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64 + b_w8 + b_w8t);
+  sc.w8 = w8 ? 1u : 0u;
+  sc.w8step = bvh.w8step;
+  sc.rw8step = 1.0f / bvh.w8step;  // a power of two: exact
   sc.cstep = bvh.cstep;
   sc.cbound = bvh.cbound;
   sc.c64step = bvh.c64step;
@@ -739,7 +800,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
   // + 1: the speculative traversal parks a second leaf on the stack (wgt_device.h)
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
-  sc.ps_waves = ps_waves_for(bvh, n_tris);
+  if (w8) sc.stack = std::max(sc.stack, bvh.w8_stack);  // the wide traversal's groups: 2 per level
+  sc.ps_waves = waves;
   // parked traversal state (WGT_PARK=0: the whole stack in LDS);
   // the LDS stack holds what fits beside the parked words at the wave budget, or the whole
   // stack when that is smaller (WGT_PS_CAP lowers it, down to kMinPsCap, for tests)
@@ -771,6 +833,11 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   in.ps_park = sc.ps_park;
   in.ps_stack = n_tris ? sc.ps_cap : 0u;
   in.bvh_c64 = c64 ? 1u : 0u;
+  fill_w8_info(bvh, w8, in);
+  {
+    const wgt_camera_param cam{{278.0f, 278.0f, -800.0f}, 0.0f, {278.0f, 278.0f, 0.0f}, 0.0f, 1.0f, 40.0f, 1u, 0u};
+    in.node_form = n_tris ? (uint32_t)node_form(sc, make_frame(cam, 1, 1)) : 0u;
+  }
   ctx->has_scene = true;
   return WGT_OK;
 }

@@ -144,10 +144,12 @@ def pad_tiles(tiles: np.ndarray, n: int):
     return np.concatenate([tiles, pad])
 
 
-def gather_tiles(local, rank: int, world: int, dist, dst: int = 0):
+def gather_tiles(local, rank: int, world: int, dist, dst: int = 0, collective: bool = False):
     """Gather equally-sized per-rank tile buffers to `dst` (RCCL gather over xGMI on
-    GPUs, gloo on CPU).  Returns the list of buffers on dst, None elsewhere."""
-    if world == 1:
+    GPUs, gloo on CPU).  Returns the list of buffers on dst, None elsewhere.  One rank
+    returns its buffer as it is unless `collective` (the call then goes through the
+    process group's gather, as at N > 1)."""
+    if world == 1 and not collective:
         return [local]
     if rank == dst:
         bufs = [local.new_empty(local.shape) for _ in range(world)]
@@ -168,15 +170,24 @@ class ShardedFrames:
     "f32" (radiance before quantisation, gathered the same way).  depth: output
     buffer sets, one per step in flight: consecutive steps launched on different
     streams (the context's pipeline streams) overlap on the device, so step k
-    renders into set k % depth (launch(stream, slot), gather(slot))."""
+    renders into set k % depth (launch(stream, slot), gather(slot)).
+
+    Decoupled gathers (gather_async, round 5): the gather and rank 0's assembly of
+    step k run on a stream of their own once step k's launch has finished, and only
+    the launch that next writes the same buffer set waits for them (wait_slot).  A
+    render launch therefore never queues behind a collective whose kernels wait for
+    CUs the next frame's persistent grid holds, and no rank's launch k + 2 is tied to
+    the slowest rank's drain of k + 1 (with depth >= 2 x the frames in flight, the
+    gather of a set has a whole step to finish before its set is written again).
+    collective: go through the process group's gather even with one rank (tests)."""
 
     def __init__(self, ctx, cam, W, H, T, frames, rank, world, dist, device, backend="nccl", want=("u8",),
-                 depth=1):
+                 depth=1, collective=False):
         import torch
 
         self.ctx, self.cam, self.W, self.H, self.T = ctx, cam, W, H, T
         self.frames, self.rank, self.world, self.dist = list(frames), rank, world, dist
-        self.backend, self.device = backend, device
+        self.backend, self.device, self.collective = backend, device, collective
         self.tiles = shard_tiles(W, H, T, self.frames, rank, world)
         self.n_max = max_tiles_per_rank(W, H, T, len(self.frames), world)
         self.d_tiles = torch.from_numpy(self.tiles.view(np.uint8).copy()).to(device)
@@ -187,6 +198,8 @@ class ShardedFrames:
                 b["f32"] = torch.zeros((self.n_max, T, T, 4), dtype=torch.float32, device=device)
             self.bufsets.append(b)
         self.bufs = self.bufsets[0]
+        self.gather_stream = None  # created on the first gather_async
+        self.done = [None] * len(self.bufsets)  # per set: an event after the gather that last read it
         self.frame_ids = [f for f, _ in self.frames]
         self.asm_idx = None
         if rank == 0:
@@ -216,9 +229,33 @@ class ShardedFrames:
 
         out = {}
         for kind, buf in self.bufsets[slot].items():
-            got = gather_tiles(buf if self.backend == "nccl" else buf.cpu(), self.rank, self.world, self.dist)
+            got = gather_tiles(buf if self.backend == "nccl" else buf.cpu(), self.rank, self.world, self.dist,
+                               collective=self.collective)
             if self.rank == 0:
-                data = (got[0] if self.world == 1 else torch.cat(got)).to(self.device).reshape(-1, 4)
+                data = (got[0] if len(got) == 1 else torch.cat(got)).to(self.device).reshape(-1, 4)
                 imgs = data[self.asm_idx]  # (frames, H, W, 4)
                 out[kind] = {f: imgs[i] for i, f in enumerate(self.frame_ids)}
         return out if self.rank == 0 else None
+
+    def wait_slot(self, stream, slot):
+        """Order `stream` (a torch stream) after the gather that last read buffer set `slot`: the
+        launch that writes the set next must not overwrite tiles still being gathered."""
+        if self.done[slot] is not None:
+            stream.wait_event(self.done[slot])
+
+    def gather_async(self, slot, after):
+        """gather(slot) on the gather stream, after everything queued so far on `after` (the
+        stream of the set's launch); records the set's done event.  Returns what gather returns:
+        rank 0's images are valid once the gather stream is synchronised (done event)."""
+        import torch
+
+        if self.gather_stream is None:
+            self.gather_stream = torch.cuda.Stream(device=self.device)
+        g = self.gather_stream
+        g.wait_stream(after)
+        with torch.cuda.stream(g):
+            out = self.gather(slot)
+            ev = torch.cuda.Event()
+            ev.record(g)
+        self.done[slot] = ev
+        return out
