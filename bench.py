@@ -497,7 +497,7 @@ def main():
             "data": f"synthetic: procedural {args.scene} stand-in ({n_tris} tris) in the reference Cornell box"
                     if args.scene != "cornell" else "synthetic: reference Cornell box",
             "config": {"workload": f"{args.scene}-{W}x{H}-{spp}spp", "width": W, "height": H, "spp": spp,
-                       "triangles": n_tris, "bvh_nodes": info["bvh_nodes"], "tile": T,
+                       "triangles": n_tris, "bvh_nodes": info["bvh_nodes"], "tile": T if world > 1 else f"{W}x{H} (one tile per frame)",
                        "frames_per_step": len(frames),
                        "parallelism": "1 GPU, no collective" if world == 1 else
                        f"tiles{world}+{'rccl' if args.dist_backend == 'nccl' else 'gloo'}-gather"},

@@ -122,8 +122,12 @@ typedef struct {
    * NaN handling, quad scan, root-node test */
   uint64_t cyc_refill, cyc_finalise, cyc_shade, cyc_camera, cyc_quads, cyc_root;
   /* persistent kernel with parked traversal state: LDS stack overflows moved to the
-   * lane's global stack, and refills from it */
+   * lane's global stack, and refills from it; with the wide form
+   * (WGT_CNODE=4): second triangle groups pushed, and taken back (§4.2 item 23) */
   uint64_t stack_spills, stack_refills;
+  /* ... and traversals ended on the global stack's overflow exit (a wrong pixel; never taken:
+   * the global stack holds the builder's bound, and the parity tests assert 0) */
+  uint64_t stack_overflows;
 } wgt_stats;
 
 typedef struct {

@@ -44,7 +44,32 @@ def test_struct_sizes_match_reference_layouts(wgt):
     assert _lib.SPHERE_DTYPE.itemsize == 32    # scene.h:47 sphere_stride_
     assert _lib.TRI_DTYPE.itemsize == 80       # scene.h:45 tri_stride_
     assert _lib.CAMERA_DTYPE.itemsize == 48    # camera.h:19-31
-    assert ctypes.sizeof(_lib.WgtStats) == 184  # + stack_spills, stack_refills (round 4)
+    assert ctypes.sizeof(_lib.WgtStats) == 192  # + stack_spills, stack_refills (round 4), stack_overflows (5)
+
+
+def test_ctypes_structs_match_the_header(tmp_path):
+    """The ctypes mirrors of wgt_stats and wgt_scene_info have the C header's size and field
+    offsets (a C program built from include/wgt_api.h with gcc prints them)."""
+    import subprocess
+
+    from webgputracer_amd import _lib
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lines = []
+    for cname, cls in (("wgt_stats", _lib.WgtStats), ("wgt_scene_info", _lib.WgtSceneInfo)):
+        lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
+        for f, _ in cls._fields_:
+            lines.append(f'printf("{cname}.{f} %zu\\n", offsetof({cname}, {f}));')
+    src = tmp_path / "sizes.c"
+    src.write_text("#include <stdio.h>\n#include <stddef.h>\n#include \"wgt_api.h\"\nint main(void) {\n" +
+                   "\n".join(lines) + "\nreturn 0;\n}\n")
+    exe = tmp_path / "sizes"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(ln.split() for ln in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines())
+    for cname, cls in (("wgt_stats", _lib.WgtStats), ("wgt_scene_info", _lib.WgtSceneInfo)):
+        assert int(got[cname]) == ctypes.sizeof(cls), cname
+        for f, _ in cls._fields_:
+            assert int(got[f"{cname}.{f}"]) == getattr(cls, f).offset, (cname, f)
 
 
 def test_version(wgt):

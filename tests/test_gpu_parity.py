@@ -29,6 +29,9 @@ def check_counters(stats, cnt, oracle):
     assert stats["queries"] == int(cnt[oracle.CNT_QUERIES])
     assert stats["samples"] == int(cnt[oracle.CNT_SAMPLES])
     assert stats["nan_rays"] == int(cnt[oracle.CNT_NAN_RAYS])
+    # the parked kernel's global stack never runs out (park_fix's overflow exit would end a
+    # traversal early: a wrong pixel)
+    assert stats["stack_overflows"] == 0
 
 
 @pytest.fixture(scope="module")

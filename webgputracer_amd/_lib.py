@@ -41,7 +41,7 @@ class WgtStats(ctypes.Structure):
                 ("cyc_refill", ctypes.c_uint64), ("cyc_finalise", ctypes.c_uint64),
                 ("cyc_shade", ctypes.c_uint64), ("cyc_camera", ctypes.c_uint64), ("cyc_quads", ctypes.c_uint64),
                 ("cyc_root", ctypes.c_uint64), ("stack_spills", ctypes.c_uint64),
-                ("stack_refills", ctypes.c_uint64)]
+                ("stack_refills", ctypes.c_uint64), ("stack_overflows", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

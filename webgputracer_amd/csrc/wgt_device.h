@@ -50,13 +50,6 @@ __device__ __forceinline__ void quad_accept(f3 o, f3 d, const float4* __restrict
 // search bound, and what finalize needs to rebuild the quad hit bit for bit.
 // EXACT: the compiler's IEEE division for t, for rays outside the render limits
 // that make div_rn exact here (k_trace's caller-supplied rays, wgt_math.h).
-// t = num / denom is rejected (t < kRayMin) whenever the signs of num and denom differ or num
-// is +-0 (IEEE division keeps the sign; the quotient is then <= -0 or +-0; div_rn too), so a
-// lane can leave before the division, and a wave whose lanes all do skips it.
-__device__ __forceinline__ bool quad_t_negative(float num, float denom) {
-  return ((__float_as_uint(num) ^ __float_as_uint(denom)) >> 31) != 0u || num == 0.0f;
-}
-
 template <bool EXACT = false>
 __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict__ q, uint32_t id,
                                            Hit& h, float& qt) {
@@ -65,7 +58,6 @@ __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict_
   if (fabs_w(denom) < kRayMin) return;
   const float4 wd = q[4];
   const float num = wd.w - dot(qn, o);
-  if (WGT_QUAD_SIGN && quad_t_negative(num, denom)) return;
   const float t = EXACT ? num / denom : div_rn(num, denom);
   if (t < kRayMin || kRayMax < t) return;
   // ray_dist is monotone non-decreasing in t >= 0 (each rounded step is), so t >=
@@ -118,63 +110,13 @@ __device__ __forceinline__ void isect_sphere(f3 o, f3 d, const float4* __restric
   h.col = xyz(col);
 }
 
-// Axis-aligned quads: normal n = s e_K (s = +-1), w = w_K e_K,
-// right = u_n e_n and up = v_m e_m on the other two axes, all with exact zeros, as the upload
-// proves per quad (wgt_runtime.cpp quad_axis_code; the device copy's pads hold the code, u_n,
-// v_m and W = +-w_K).  Then every step of the reference's isect_quad has exactly-zero terms:
-// dot(n, d) = s d_K and dot(n, o) = s o_K (adding +-0 to a nonzero is exact; a zero result only
-// differs in its sign, which no test sees), and the edge coordinates a = dot(w, cross(hit_vec,
-// up)) and b = dot(w, cross(right, hit_vec)) are w_K times one rounded product each, a = (h_ia
-// v_m) W and b = (u_n h_ib) W (a sign changes no rounding): the same t, ray_dist, a and b bit
-// for bit, in about half the VALU (tests/test_quad_axis.py checks the arithmetic).
-template <int K>
-__device__ __forceinline__ float comp(f3 v) { return K == 0 ? v.x : (K == 1 ? v.y : v.z); }
-template <int K>
-__device__ __forceinline__ void isect_quad_axis(f3 o, f3 d, const float4* __restrict__ q, uint32_t id, Hit& h,
-                                                float& qt, uint32_t code) {
-  const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-  const float s = (code & 16u) ? -1.0f : 1.0f;
-  const float denom = s * comp<K>(d);
-  if (fabs_w(denom) < kRayMin) return;
-  const float num = q[4].w - s * comp<K>(o);
-  if (WGT_QUAD_SIGN && quad_t_negative(num, denom)) return;
-  const float t = div_rn(num, denom);
-  if (t < kRayMin || kRayMax < t) return;
-  if (t >= qt) return;  // see isect_quad
-  const f3 pos = o + t * d;
-  const float ray_dist = distance(pos, o);
-  if (ray_dist >= h.dist) return;
-  const float h1 = comp<(K + 1) % 3>(pos) - comp<(K + 1) % 3>(xyz(q0));
-  const float h2 = comp<(K + 2) % 3>(pos) - comp<(K + 2) % 3>(xyz(q0));
-  const bool swap = (code & 8u) != 0u;
-  const float a = ((swap ? h2 : h1) * q2.w) * q3.w;
-  const float b = (q1.w * (swap ? h1 : h2)) * q3.w;
-  if ((__builtin_fminf(a, b) < 0.0f) || (1.0f < __builtin_fmaxf(a, b))) return;
-  quad_accept(o, d, q, id, t, ray_dist, h);
-  qt = t;
-}
-
 template <bool EXACT = false>
 __device__ __forceinline__ void quad_scan(const DevScene& sc, f3 o, f3 d, Hit& h, float& qt) {
   hit_init(h);
   qt = __builtin_inff();
   const uint32_t nlq = sc.n_lights + sc.n_quads;
   for (uint32_t k = 0; k < nlq; ++k) {
-    const float4* __restrict__ q = sc.quads + 6 * k;
-#if WGT_QUAD_AXIS
-    // code (the device copy's pos.w): 0 = general, else 1 | K << 1 | swap << 3 (wave-uniform)
-    const uint32_t code = EXACT ? 0u : __float_as_uint(q[0].w);
-    if (code & 1u) {
-      const uint32_t axis = (code >> 1) & 3u;
-      if (axis == 0u) isect_quad_axis<0>(o, d, q, k, h, qt, code);
-      else if (axis == 1u) isect_quad_axis<1>(o, d, q, k, h, qt, code);
-      else isect_quad_axis<2>(o, d, q, k, h, qt, code);
-    } else {
-      isect_quad<EXACT>(o, d, q, k, h, qt);
-    }
-#else
-    isect_quad<EXACT>(o, d, q, k, h, qt);
-#endif
+    isect_quad<EXACT>(o, d, sc.quads + 6 * k, k, h, qt);
   }
 }
 
@@ -201,6 +143,7 @@ __device__ __forceinline__ void nan_hit(const DevScene& sc, f3 o, f3 d, Hit& h) 
 struct TravStats {
   uint32_t nodes, tris, wave_steps, lane_steps;
   uint32_t spills, refills;  // parked k_render_ps: global-stack moves (park_fix)
+  uint32_t overflows;        // parked k_render_ps: park_fix's overflow exit (never taken: tests assert 0)
 };
 
 // Counts one per wave (first active lane) and one per active lane.
@@ -1092,6 +1035,7 @@ __device__ __forceinline__ void flush_counters(unsigned long long* __restrict__ 
   atomicAdd(&counters[CNT_TRAV_LANE], (unsigned long long)st.lane_steps);
   if (st.spills) atomicAdd(&counters[CNT_STACK_SPILLS], (unsigned long long)st.spills);
   if (st.refills) atomicAdd(&counters[CNT_STACK_REFILLS], (unsigned long long)st.refills);
+  if (st.overflows) atomicAdd(&counters[CNT_STACK_OVERFLOWS], (unsigned long long)st.overflows);
 }
 
 

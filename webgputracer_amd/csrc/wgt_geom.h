@@ -109,16 +109,6 @@ constexpr uint32_t kTriRecordBytes = WGT_TRI_REC;
 // triangles tested per triangle step of the phase-split kernel (wgt_device.h tri_step): two
 // measured -1.6% on sponza, -1.3% on bunny at 1080p/256 spp; three and four +6%/+13% on sponza
 // (profiles/sweeps/r03_ab_tri_per_step.log)
-// the axis-aligned quad path of the render kernels' quad scan (wgt_device.h isect_quad_axis)
-// and the sign pre-rejection before the quad division (quad_t_negative): both exact, both
-// measured slower (sponza -1.1 % / -1.0 %, bunny -2.8 % / -0.7 %, profiles/r04/quad_axis_ab.log),
-// so off by default
-#ifndef WGT_QUAD_AXIS
-#define WGT_QUAD_AXIS 0
-#endif
-#ifndef WGT_QUAD_SIGN
-#define WGT_QUAD_SIGN 0
-#endif
 #ifndef WGT_TRI_PER_STEP
 #define WGT_TRI_PER_STEP 2
 #endif

@@ -174,6 +174,7 @@ enum {
   CNT_CYC_ROOT,
   CNT_STACK_SPILLS,   // parked k_render_ps: LDS stack overflows moved to the global stack
   CNT_STACK_REFILLS,  // ... and refills from it
+  CNT_STACK_OVERFLOWS,  // ... and traversals park_fix ended on its overflow exit (a wrong pixel)
   CNT_N = 24
 };
 

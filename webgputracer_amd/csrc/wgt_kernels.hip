@@ -237,6 +237,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             if (STATS) {
               st.spills += k == 1u ? 1u : 0u;
               st.refills += k == 2u ? 1u : 0u;
+              st.overflows += k == 3u ? 1u : 0u;
             }
             pending = false;
             trav = true;

@@ -175,8 +175,10 @@ bool c64_fits(const BvhOut& bvh) {
 // stack holds what fits beside the parked words at the wave budget,
 // or the whole stack (`stack` entries) when that is smaller; WGT_PS_CAP lowers it, down to
 // kMinPsCap, for tests.
+// 7 waves per SIMD park (the only form of that budget); a WGT_PS_WAVES=7 request that the tree cannot
+// take (ps_waves_for gave 6 or 5) does not park unless WGT_PARK asks for it.
 void ps_park_cap(uint32_t n_tris, uint32_t stack, uint32_t waves, uint32_t& park, uint32_t& cap) {
-  park = n_tris > 0 && (env_u32("WGT_PARK", 0) || env_u32("WGT_PS_WAVES", 0) == 7) ? 1u : 0u;
+  park = n_tris > 0 && (env_u32("WGT_PARK", 0) || waves == 7) ? 1u : 0u;
   cap = stack;
   if (!park) return;
   uint32_t c = std::min(stack, ps_cap_max(waves));
@@ -291,42 +293,6 @@ std::string check_scene_limits(const wgt_quad* lq, uint32_t nlq, const wgt_spher
 
 double sq(double x) { return x * x; }
 
-// The axis-aligned form of a light/quad record for the kernels' quad scan (wgt_device.h
-// isect_quad_axis), written into the device copy's pads (the reference
-// kernels read only .xyz of these): pos.w = code, right.w = u_n, up.w = v_m, norm.w = W.
-// code = 1 | K << 1 | swap << 3 | (s < 0) << 4 when norm = s e_K (s = +-1, exact zeros),
-// w = w_K e_K, up = v_m e_m and right = u_n e_n on the two other axes (exact zeros), every
-// value finite; else 0 (the general path).  With K1 = K+1, K2 = K+2 (mod 3), up along K2
-// gives a = (h_K1 v_m) w_K and b = (u_n h_K2) w_K; up along K1 (swap) a = (h_K2 v_m)(-w_K) and
-// b = (u_n h_K1)(-w_K): W = w_K, or -w_K with swap.
-void quad_axis_code(const wgt_quad& q, float pads[4]) {
-  pads[0] = pads[1] = pads[2] = pads[3] = 0.0f;
-  auto axis_of = [](const float* v, float& val) {  // the one nonzero component, or -1
-    int ax = -1;
-    for (int c = 0; c < 3; ++c) {
-      if (!std::isfinite(v[c])) return -1;
-      if (v[c] != 0.0f) {
-        if (ax >= 0) return -1;
-        ax = c;
-        val = v[c];
-      }
-    }
-    return ax;
-  };
-  float s = 0.0f, u = 0.0f, v = 0.0f, wk = 0.0f;
-  const int k = axis_of(q.norm, s);
-  if (k < 0 || (s != 1.0f && s != -1.0f)) return;
-  if (axis_of(q.w, wk) != k) return;
-  const int m = axis_of(q.up, v), n = axis_of(q.right, u);
-  if (m < 0 || n < 0 || m == k || n == k || m == n || !std::isfinite(q.d)) return;
-  const bool swap = m == (k + 1) % 3;
-  const uint32_t code = 1u | (uint32_t)k << 1 | (swap ? 8u : 0u) | (s < 0.0f ? 16u : 0u);
-  std::memcpy(&pads[0], &code, 4);
-  pads[1] = u;
-  pads[2] = v;
-  pads[3] = swap ? -wk : wk;
-}
-
 // Largest |coordinate| any point of the scene's primitives can have (quad corners,
 // sphere boxes, triangle vertices): hit points, i.e. secondary ray origins, lie
 // within it.  The compact nodes are built for ray origins within 4x this bound,
@@ -399,6 +365,7 @@ void fill_stats(const unsigned long long* c, wgt_stats* s) {
   s->cyc_root = c[CNT_CYC_ROOT];
   s->stack_spills = c[CNT_STACK_SPILLS];
   s->stack_refills = c[CNT_STACK_REFILLS];
+  s->stack_overflows = c[CNT_STACK_OVERFLOWS];
 }
 
 
@@ -740,15 +707,6 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   std::vector<char> host(total, 0);
   std::memcpy(host.data(), lights, (size_t)n_lights * 96);
   if (n_quads) std::memcpy(host.data() + (size_t)n_lights * 96, quads, (size_t)n_quads * 96);
-  for (uint32_t i = 0; i < nlq; ++i) {  // the axis-aligned form in the device copy's pads
-    wgt_quad* dq = reinterpret_cast<wgt_quad*>(host.data() + (size_t)i * 96);
-    float pads[4];
-    quad_axis_code(*dq, pads);
-    dq->pos[3] = pads[0];
-    dq->right[3] = pads[1];
-    dq->up[3] = pads[2];
-    dq->norm[3] = pads[3];
-  }
   std::memcpy(host.data() + b_quads, spheres, (size_t)n_spheres * 32);
   if (n_tris) {
     std::memcpy(host.data() + b_quads + b_sph, bvh.nodes.data(), bvh.nodes.size() * 4);
@@ -802,6 +760,9 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
   if (w8) sc.stack = std::max(sc.stack, bvh.w8_stack);  // the wide traversal's groups: 2 per level
   sc.ps_waves = waves;
+  if (env_u32("WGT_PS_WAVES", 0) == 7 && waves != 7 && env_u32("WGT_DEBUG", 0))
+    std::fprintf(stderr, "[wgt] WGT_PS_WAVES=7: the tree's refs do not fit 3-byte stack entries; %u waves per SIMD\n",
+                 waves);
   // parked traversal state (WGT_PARK=0: the whole stack in LDS);
   // the LDS stack holds what fits beside the parked words at the wave budget, or the whole
   // stack when that is smaller (WGT_PS_CAP lowers it, down to kMinPsCap, for tests)

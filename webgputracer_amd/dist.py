@@ -188,28 +188,38 @@ class ShardedFrames:
         self.ctx, self.cam, self.W, self.H, self.T = ctx, cam, W, H, T
         self.frames, self.rank, self.world, self.dist = list(frames), rank, world, dist
         self.backend, self.device, self.collective = backend, device, collective
-        self.tiles = shard_tiles(W, H, T, self.frames, rank, world)
-        self.n_max = max_tiles_per_rank(W, H, T, len(self.frames), world)
+        # one rank (no collective): each frame is one W x H tile, whose compact output is the frame
+        # itself, row-major: nothing to gather and nothing to assemble
+        self.whole = world == 1 and not collective
+        self.tw, self.th = (W, H) if self.whole else (T, T)
+        if self.whole:
+            self.tiles = np.zeros(len(self.frames), TILE_DTYPE)
+            self.tiles["seed"] = [seed & 0xFFFFFFFF for _, seed in self.frames]
+            self.tiles["frame"] = [fid for fid, _ in self.frames]
+            self.n_max = len(self.frames)
+        else:
+            self.tiles = shard_tiles(W, H, T, self.frames, rank, world)
+            self.n_max = max_tiles_per_rank(W, H, T, len(self.frames), world)
         self.d_tiles = torch.from_numpy(self.tiles.view(np.uint8).copy()).to(device)
         self.bufsets = []
         for _ in range(max(depth, 1)):
-            b = {"u8": torch.zeros((self.n_max, T, T, 4), dtype=torch.uint8, device=device)}
+            b = {"u8": torch.zeros((self.n_max, self.th, self.tw, 4), dtype=torch.uint8, device=device)}
             if "f32" in want:
-                b["f32"] = torch.zeros((self.n_max, T, T, 4), dtype=torch.float32, device=device)
+                b["f32"] = torch.zeros((self.n_max, self.th, self.tw, 4), dtype=torch.float32, device=device)
             self.bufsets.append(b)
         self.bufs = self.bufsets[0]
         self.gather_stream = None  # created on the first gather_async
         self.done = [None] * len(self.bufsets)  # per set: an event after the gather that last read it
         self.frame_ids = [f for f, _ in self.frames]
         self.asm_idx = None
-        if rank == 0:
+        if rank == 0 and not self.whole:
             layout = self.tiles if world == 1 else np.concatenate(
                 [pad_tiles(shard_tiles(W, H, T, self.frames, r, world), self.n_max) for r in range(world)])
             self.asm_idx = torch.from_numpy(assemble_index(layout, W, H, T, self.frame_ids)).to(device)
 
     def stats(self):
         """Instrumented pass over this rank's tiles (exact counters; untimed)."""
-        return self.ctx.render_tiles_stats(self.cam, self.W, self.H, self.T, self.T, self.d_tiles.data_ptr(),
+        return self.ctx.render_tiles_stats(self.cam, self.W, self.H, self.tw, self.th, self.d_tiles.data_ptr(),
                                            len(self.tiles))
 
     def launch(self, stream=0, slot=0):
@@ -217,7 +227,7 @@ class ShardedFrames:
         hipStream_t)."""
         bufs = self.bufsets[slot]
         f32 = bufs.get("f32")
-        self.ctx.render_tiles_async(self.cam, self.W, self.H, self.T, self.T, self.d_tiles.data_ptr(),
+        self.ctx.render_tiles_async(self.cam, self.W, self.H, self.tw, self.th, self.d_tiles.data_ptr(),
                                     len(self.tiles), d_u8=bufs["u8"].data_ptr(),
                                     d_f32=f32.data_ptr() if f32 is not None else 0, stream=stream)
 
@@ -229,6 +239,9 @@ class ShardedFrames:
 
         out = {}
         for kind, buf in self.bufsets[slot].items():
+            if self.whole:  # the frames themselves (views of the output set)
+                out[kind] = {f: buf[i] for i, f in enumerate(self.frame_ids)}
+                continue
             got = gather_tiles(buf if self.backend == "nccl" else buf.cpu(), self.rank, self.world, self.dist,
                                collective=self.collective)
             if self.rank == 0:
