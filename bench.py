@@ -116,21 +116,28 @@ N_SIMDS = 256 * 4     # MI355X: 256 CUs x 4 SIMDs (MI355X_MICROARCH.md)
 VALU_ISSUE_CYCLES = 2  # cycles of a wave64 f32 VALU instruction on a SIMD-32 (MI355X_MICROARCH.md)
 
 
-def sq_fields(agg, calls):
+def sq_fields(agg, calls, grid_waves=None):
     """VALU-busy fraction and the wave-cycle split of the kernel from the SQ pass: waves are
     issuing (SQ_ACTIVE_INST_ANY), parked in s_waitcnt (SQ_WAIT_ANY) or ready but not issued
     (SQ_WAIT_INST_ANY); the three are disjoint and sum to SQ_WAVE_CYCLES (MI355X_MICROARCH.md
     §rocprofv3).  A persistent launch keeps its waves for the whole launch, so the launch
-    lasts ~4 x SQ_WAVE_CYCLES / SQ_WAVES cycles (SQ_WAVE_CYCLES counts quad-cycles) and the
-    VALU pipes are busy SQ_INSTS_VALU x 2 cycles / (SIMDs x that)."""
+    lasts ~4 x SQ_WAVE_CYCLES / waves cycles (SQ_WAVE_CYCLES counts quad-cycles) and the
+    VALU pipes are busy SQ_INSTS_VALU x 2 cycles / (SIMDs x that).  waves = the launch's grid
+    (grid_waves, known to the caller) when given: SQ_WAVES read twice the grid on bunny's
+    one-dispatch pass in round 5 (12,288 for 6,144 waves; sponza's pass counted 6,144) while
+    SQ_WAVE_CYCLES matched the grid, so it is kept in `raw` only."""
     wc = agg.get("SQ_WAVE_CYCLES", 0.0)
-    waves = agg.get("SQ_WAVES", 0.0)
+    sq_waves = agg.get("SQ_WAVES", 0.0)
+    waves = float(grid_waves) * calls if grid_waves else sq_waves
     if wc <= 0 or waves <= 0:
         return None
     launch_cycles = 4.0 * wc / waves
     valu = agg.get("SQ_INSTS_VALU", 0.0) / calls
     return {"valu_busy": round(valu * VALU_ISSUE_CYCLES / (N_SIMDS * launch_cycles), 4),
             "valu_insts_per_launch": valu,
+            # the raw figures (per launch), for auditing the two ratios
+            "raw": {"SQ_WAVES": sq_waves / calls, "grid_waves": waves / calls, "SQ_WAVE_CYCLES": wc / calls,
+                    "SQ_INSTS_VALU": valu, "dispatches": calls},
             "wave_split": {"issuing": round(agg.get("SQ_ACTIVE_INST_ANY", 0.0) / wc, 4),
                            "waiting": round(agg.get("SQ_WAIT_ANY", 0.0) / wc, 4),
                            "issue_stalled": round(agg.get("SQ_WAIT_INST_ANY", 0.0) / wc, 4)}}
@@ -149,7 +156,7 @@ def limiter(hbm_frac, sq):
     return "latency"
 
 
-def live_pmc(args, kernel):
+def live_pmc(args, kernel, grid_waves=None):
     """HBM bytes and L2 requests per launch of `kernel`, measured now on this device and binary:
     one rocprofv3 --pmc pass per counter group (never combined with traces; each pass within the
     per-block counter limits, under its own kill timeout) over a child run of this script that
@@ -206,7 +213,8 @@ def live_pmc(args, kernel):
     req = (agg.get("TCC_HIT_sum", 0.0) + agg.get("TCC_MISS_sum", 0.0)) / calls
     hit = agg.get("TCC_HIT_sum", 0.0) / max(agg.get("TCC_HIT_sum", 0.0) + agg.get("TCC_MISS_sum", 0.0), 1.0)
     return {"hbm_bytes_per_launch": hbm, "tcc_requests_per_launch": req, "tcc_hit_rate": round(hit, 4),
-            "write_bytes_per_launch": agg.get("WRITE_SIZE", 0.0) * 1024.0 / calls, "sq": sq_fields(agg, calls)}, \
+            "write_bytes_per_launch": agg.get("WRITE_SIZE", 0.0) * 1024.0 / calls,
+            "sq": sq_fields(agg, calls, grid_waves)}, \
         f"live: {len(PMC_PASSES)} rocprofv3 --pmc passes of one frame of this workload alone, this run"
 
 
@@ -463,7 +471,11 @@ def main():
         # live PMC passes of this binary on this device (N = 1), in place of the profile entry
         traffic_source = "profile" if traffic is not None else None
         if world == 1 and (args.pmc == "on" or (args.pmc == "auto" and args.steps > 0)):
-            live, note = live_pmc(args, kernel)
+            # the child renders one whole W x H frame at N = 1: its persistent grid is the device's
+            # resident capacity or one wave per 8x8 pixel block, whichever is smaller
+            res = int(info.get("ps_resident", 0))
+            grid = min(((W + 7) // 8) * ((H + 7) // 8), res) if res else None
+            live, note = live_pmc(args, kernel, grid)
             if live is not None:
                 traffic, tj_id, traffic_note, traffic_source = live["hbm_bytes_per_launch"], build_id, note, "live"
                 sq, write_b = live["sq"], live["write_bytes_per_launch"]
@@ -504,6 +516,7 @@ def main():
             "samples_per_s": round(samples / max_t, 1),
             "reference_queries_per_s": round(queries / max_t, 1),
             "kernel_ms": round(kern_ms, 3),
+            "persistent_grid_waves": int(info.get("ps_resident", 0)),
             "timing": {"pipeline": P,
                        "launch_ms": round(kern_ms, 3),
                        "launch_ms_is": "event pair around each launch" if P == 1 or args.steps < 2 else
@@ -529,6 +542,7 @@ def main():
                          # but not issued (sq_fields)
                          "valu_busy": sq["valu_busy"] if sq else None,
                          "wave_split": sq["wave_split"] if sq else None,
+                         "sq_raw": sq.get("raw") if sq else None,
                          "bytes_per_unit": {"node": SURVEY_NODE_BYTES, "tri": SURVEY_TRI_BYTES,
                                             "shade_per_ray": SHADE_BYTES},
                          # the bytes this implementation's encodings load per launch (80-B compact or 112-B

@@ -157,6 +157,7 @@ typedef struct {
   float w8_bound;         /* wgt_bvh_build_wide: the codes hold for ray origins within this bound */
   uint32_t node_form;     /* node form of the persistent kernel for the reference camera: 0 = 128-B,
                            * 1 = 80-B compact, 2 = 64-B compact, 3 = wide (WGT_CNODE) */
+  uint32_t ps_resident;   /* waves of the persistent grid (the device's resident capacity) */
 } wgt_scene_info;
 
 typedef struct wgt_ctx wgt_ctx;

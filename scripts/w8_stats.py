@@ -17,7 +17,7 @@ for cn in os.environ.get("W8_FORMS", "2 4").split():
     info = ctx.scene_info()
     st = ctx.render_tile(w.camera_param(W / H, spp, 0), W, H, want=(), stats=True)["stats"]
     r = max(st["traced_rays"], 1)
-    print(json.dumps({"scene": scene, "cnode": cn, "node_form": info["node_form"], 
+    print(json.dumps({"scene": scene, "cnode": cn, "node_form": info["node_form"], "ps_resident": info["ps_resident"], 
                       "kernel_ms": round(st["kernel_ms"], 3), "nodes_per_ray": round(st["node_visits"] / r, 4),
                       "tris_per_ray": round(st["tri_tests"] / r, 4),
                       "tri_groups_pushed_per_ray": round(st["stack_spills"] / r, 4),

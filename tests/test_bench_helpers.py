@@ -28,6 +28,20 @@ def test_sq_fields_round3_profile():
     assert bench.sq_fields({}, 1) is None
 
 
+def test_sq_fields_grid_waves_round5_bunny():
+    """Round 5's bunny pass (one dispatch of a 6,144-wave persistent grid): SQ_WAVES read 12,288,
+    SQ_WAVE_CYCLES 357.3e9 quad-cycles, SQ_INSTS_VALU 84.8e9.  Taken from the grid, the launch
+    length gives VALU pipes busy ~0.71 (round 4's figure); from SQ_WAVES it read 1.42, an
+    impossible fraction.  SQ_WAVES is kept in `raw`."""
+    agg = {"SQ_WAVES": 12288.0, "SQ_WAVE_CYCLES": 357326536227.0, "SQ_INSTS_VALU": 84808015695.0,
+           "SQ_WAIT_ANY": 0.32 * 357326536227.0, "SQ_WAIT_INST_ANY": 0.3268 * 357326536227.0,
+           "SQ_ACTIVE_INST_ANY": 0.3532 * 357326536227.0}
+    sq = bench.sq_fields(agg, 1, grid_waves=6144)
+    assert 0.70 < sq["valu_busy"] < 0.72
+    assert sq["raw"]["SQ_WAVES"] == 12288.0 and sq["raw"]["grid_waves"] == 6144.0
+    assert bench.sq_fields(agg, 1)["valu_busy"] > 1.0  # the SQ_WAVES form
+
+
 def test_limiter():
     assert bench.limiter(0.8, None) == "hbm"
     assert bench.limiter(0.375, {"valu_busy": 0.75}) == "valu"

@@ -58,7 +58,8 @@ class WgtSceneInfo(ctypes.Structure):
                 ("bvh_w8", ctypes.c_uint32), ("w8_groups", ctypes.c_uint32), ("w8_nodes", ctypes.c_uint32),
                 ("w8_leaves", ctypes.c_uint32), ("w8_depth", ctypes.c_uint32), ("w8_stack", ctypes.c_uint32),
                 ("w8_step", ctypes.c_float), ("w8_sah", ctypes.c_double), ("w8_records", ctypes.c_uint32),
-                ("w8_bound", ctypes.c_float), ("node_form", ctypes.c_uint32)]
+                ("w8_bound", ctypes.c_float), ("node_form", ctypes.c_uint32),
+                ("ps_resident", ctypes.c_uint32)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -799,6 +799,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     const wgt_camera_param cam{{278.0f, 278.0f, -800.0f}, 0.0f, {278.0f, 278.0f, 0.0f}, 0.0f, 1.0f, 40.0f, 1u, 0u};
     in.node_form = n_tris ? (uint32_t)node_form(sc, make_frame(cam, 1, 1)) : 0u;
   }
+  in.ps_resident = ctx->ps_resident;
   ctx->has_scene = true;
   return WGT_OK;
 }
