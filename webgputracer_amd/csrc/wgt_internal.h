@@ -186,10 +186,12 @@ enum {
 // order (one launch in flight per workspace): the queues, the LPT costs and order, and the
 // parked kernel's global stacks.
 size_t render_ws_bytes(const DevScene& sc, const DevFrame& fr, uint32_t resident);
+// ws_clean_nb: in, the block count whose queues and costs the workspace's previous LPT launch left
+// zero (0: unknown, a memset clears them); out, the same for this launch
 hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
                          uchar4* out8, float4* out32, uint32_t* outhit,
                          unsigned long long* counters, uint32_t resident, void* ws, size_t ws_cap,
-                         hipStream_t stream);
+                         hipStream_t stream, uint32_t& ws_clean_nb);
 // The node form k_render_ps reads for this scene and frame (DevFrame::cnode): 0 = 128-B
 // nodes, 1 = 80-B compact records, 2 = 64-B compact records.
 int node_form(const DevScene& sc, const DevFrame& fr);

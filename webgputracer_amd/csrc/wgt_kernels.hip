@@ -412,11 +412,16 @@ k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __res
 // LPT order of the pixel blocks from the pre-pass costs, one workgroup: bucket
 // by the float bits of the cost (exponent + 3 mantissa bits: 8 buckets per
 // octave), most expensive bucket first (order within a bucket is arbitrary: the
-// order only shapes the schedule, never a pixel's result).
-constexpr int kLptThreads = 1024, kLptBuckets = 1280;  // float bits >> 20 of any u32 cost
+// order only shapes the schedule, never a pixel's result).  It also leaves the launch's
+// scheduling words as the next launch on the same workspace needs them (launch_render): the
+// costs it has read zeroed, and both queue counters zeroed (the pre-pass's is done; the main
+// kernel's starts after this kernel), so that no memset kernel runs per frame.  256 threads: a
+// workgroup that finds room on a CU while the previous frame's persistent grid drains (1,024
+// threads needed 16 free wave slots on one CU).
+constexpr int kLptThreads = 256, kLptBuckets = 1280;  // float bits >> 20 of any u32 cost
 __device__ __forceinline__ uint32_t lpt_bucket(uint32_t c) { return __float_as_uint((float)c) >> 20; }
 __global__ void __launch_bounds__(kLptThreads)
-k_lpt_order(const uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __restrict__ perm) {
+k_lpt_order(uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __restrict__ perm, uint32_t* __restrict__ queues) {
   __shared__ uint32_t s_cnt[kLptBuckets];
   for (int b = threadIdx.x; b < kLptBuckets; b += kLptThreads) s_cnt[b] = 0;
   __syncthreads();
@@ -429,9 +434,15 @@ k_lpt_order(const uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __rest
       s_cnt[b] = run;
       run += n;
     }
+    queues[0] = 0u;  // the pre-pass's queue (finished)
+    queues[1] = 0u;  // the main kernel's queue (next in stream order)
   }
   __syncthreads();
-  for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) perm[atomicAdd(&s_cnt[lpt_bucket(cost[i])], 1u)] = i;
+  for (uint32_t i = threadIdx.x; i < blocks; i += kLptThreads) {
+    const uint32_t c = cost[i];
+    cost[i] = 0u;
+    perm[atomicAdd(&s_cnt[lpt_bucket(c)], 1u)] = i;
+  }
 }
 
 // wgt_selftest_math: the kernels' sqrt / division forms (wgt_math.h) against
@@ -581,7 +592,7 @@ size_t render_ws_bytes(const DevScene& sc, const DevFrame& fr, uint32_t resident
 hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile* d_tiles,
                          uchar4* out8, float4* out32, uint32_t* outhit,
                          unsigned long long* counters, uint32_t resident, void* ws, size_t ws_cap,
-                         hipStream_t stream) {
+                         hipStream_t stream, uint32_t& ws_clean_nb) {
   const uint32_t bx = (fr.tw + 7u) / 8u, by = (fr.th + 7u) / 8u;
   const uint64_t blocks = (uint64_t)bx * by * fr.n_tiles;
   if (blocks == 0) return hipSuccess;
@@ -613,7 +624,9 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
     const uint64_t sched = (256 + 8ull * nb + 255) & ~255ull;
     f.ps_spill = ps_spill_bytes(sc, resident) ? (int*)((char*)ws + sched) : nullptr;
     f.ps_spill_stride = grid.x * kBlock;
-    hipError_t e = hipMemsetAsync(ws, 0, 256 + (lpt ? 4ull * nb : 0), stream);
+    // the queues and costs start at zero: a memset, unless the previous LPT launch on this workspace
+    // had the same block count and left them zero (k_lpt_order; ws_clean_nb = nb)
+    hipError_t e = lpt && ws_clean_nb == nb ? hipSuccess : hipMemsetAsync(ws, 0, 256 + (lpt ? 4ull * nb : 0), stream);
     if (e == hipSuccess && lpt) {
       DevFrame fc = f;  // the pre-pass: fr.pq_lpt^2 samples per pixel
       fc.sqrt_spp = fr.pq_lpt < fr.sqrt_spp ? fr.pq_lpt : fr.sqrt_spp;
@@ -623,7 +636,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       fc.cost = (uint32_t*)((char*)ws + 256);
       fc.n_slots = nb * (fr.pq_lpt_all ? 64u : 16u);  // by default a quarter of each block's pixels estimate its cost
       ps_launch<false, true>(sc, cn, grid, block, plds, stream, fc, d_tiles, nullptr, nullptr, nullptr, nullptr, q);
-      k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb);
+      k_lpt_order<<<1, kLptThreads, 0, stream>>>(fc.cost, nb, fc.cost + nb, q);
       f.perm = fc.cost + nb;
       e = hipGetLastError();
     }
@@ -632,6 +645,8 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
       else ps_launch<false, false>(sc, cn, grid, block, plds, stream, f, d_tiles, out8, out32, outhit, nullptr, q + 1);
       e = hipGetLastError();
     }
+    // after an LPT launch k_lpt_order has left the queues and nb costs zero for the next one
+    ws_clean_nb = e == hipSuccess && lpt ? nb : 0u;
     return e;
   }
   const dim3 grid((uint32_t)blocks);

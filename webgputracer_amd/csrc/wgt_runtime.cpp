@@ -56,6 +56,7 @@ struct wgt_ctx {
   struct WsSlot {
     DevBuf ws;
     hipEvent_t ev = nullptr;  // recorded after the slot's last launch
+    uint32_t clean_nb = 0;    // launch_render: the block count its last LPT launch left zero
   };
   WsSlot slots[kMaxWsSlots];
   uint32_t next_slot = 0;
@@ -405,11 +406,19 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
   ctx->next_slot = (ctx->next_slot + 1) % n_slots;
   const size_t ws_need = render_ws_bytes(ctx->sc, fr, ctx->ps_resident);
   if (sl.ws.bytes < ws_need && (rc = use_drain(ctx))) return rc;  // before regrowing
+  const void* old_ws = sl.ws.p;
   if ((rc = ensure(ctx, sl.ws, ws_need))) return rc;
+  if (sl.ws.p != old_ws) sl.clean_nb = 0;  // a new workspace: nothing is known zero
   if (!sl.ev) WGT_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
   else WGT_HIP(ctx, hipStreamWaitEvent(s, sl.ev, 0));
-  WGT_HIP(ctx, launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
-                             sl.ws.p, sl.ws.bytes, s));
+  {
+    const hipError_t e = launch_render(ctx->sc, fr, d_tiles, out8, out32, outhit, counters, ctx->ps_resident,
+                                       sl.ws.p, sl.ws.bytes, s, sl.clean_nb);
+    if (e != hipSuccess) {
+      sl.clean_nb = 0;
+      return fail(ctx, WGT_E_HIP, std::string("launch_render: ") + hipGetErrorString(e));
+    }
+  }
   WGT_HIP(ctx, hipEventRecord(sl.ev, s));
   if (timing) {
     WGT_HIP(ctx, hipEventRecord(e1, s));
