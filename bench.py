@@ -59,8 +59,6 @@ def dominant_kernel(form: int, waves: int, tris: bool = True, park: bool = True)
     triangles runs the 8-wave instantiation without traversal)."""
     if not tris:
         return "wgt::k_render_ps<false, false, 0, 8, false, false>"
-    if waves == 4:  # two pixels per lane (WGT_PS_WAVES=4)
-        return f"wgt::k_render_ps2<false, false, {int(form)}>"
     return f"wgt::k_render_ps<false, false, {int(form)}, {waves}, true, {'true' if park else 'false'}>"
 
 

@@ -1,3 +1,4 @@
+# Historical (round 5): k_render_ps2 / WGT_PS_WAVES=4 / WGT_PX2_* were removed after commit 050a6a2.
 # Round 5: two pixels per lane (WGT_PS_WAVES=4, k_render_ps2) on the GPU: parity subset, then the
 # driver's bench command per variant (same box).  Usage: bash scripts/gpu_r05_px2.sh TAG [steps]
 # VARIANTS: space-separated name=ENV,ENV (ENV as K:V), e.g. "base= px2=WGT_PS_WAVES:4"

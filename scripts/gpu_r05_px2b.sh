@@ -1,3 +1,4 @@
+# Historical (round 5): k_render_ps2 / WGT_PS_WAVES=4 / WGT_PX2_* were removed after commit 050a6a2.
 # Round 5: why two pixels per lane is slow: STATS counters per variant, then the bench with live
 # PMC passes (VALU instructions, wave-cycle split) for the default and the two-pixel kernel.
 set -o pipefail

@@ -1,3 +1,4 @@
+# Historical (round 5): k_render_ps2 / WGT_PS_WAVES=4 / WGT_PX2_* were removed after commit 050a6a2.
 # Round 5: two pixels per lane, diagnostics: STATS counters at 16 and 256 spp (bunny).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp

@@ -1,3 +1,4 @@
+# Historical (round 5): k_render_ps2 / WGT_PS_WAVES=4 / WGT_PX2_* were removed after commit 050a6a2.
 # Round 5: two pixels per lane, diagnosis: per 4-wave form (WGT_PX2_MODE 0 = two pixels per lane,
 # 1 = k_render_ps2 with one, 2 = k_render_ps at 4 waves) and the default, the frame time and STATS
 # counters, then one rocprofv3 --pmc pass of the instruction mix per form.

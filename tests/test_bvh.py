@@ -264,11 +264,6 @@ def test_wave_budget_and_narrow_tree(monkeypatch):
     monkeypatch.delenv("WGT_NARROW")
     info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
     assert info["ps_waves"] == 5 and info["bvh_stack"] == 31
-    # two pixels per lane (k_render_ps2): 4 waves, 4-byte entries, never parked
-    monkeypatch.setenv("WGT_PS_WAVES", "4")
-    monkeypatch.setenv("WGT_PARK", "1")
-    info, _, _ = w.bvh_build(w.procedural_mesh("bunny"))
-    assert info["ps_waves"] == 4 and info["ps_park"] == 0 and info["ps_stack"] == info["bvh_stack"] + 1
 
 
 def stack24_roundtrip(v):

@@ -282,9 +282,8 @@ _FULL = {}
 
 @pytest.mark.parametrize("kind,spp,env", [("sponza", 4, {}), ("sponza", 4, {"WGT_CNODE": "3"}),
                                           ("sponza", 4, {"WGT_PARK": "1"}), ("sponza", 4, {"WGT_PS_WAVES": "7"}),
-                                          ("sponza", 4, {"WGT_CNODE": "4"}), ("sponza", 4, {"WGT_PS_WAVES": "4"}),
-                                          ("bunny", 1, {}), ("bunny", 1, {"WGT_CNODE": "4"}),
-                                          ("bunny", 1, {"WGT_PS_WAVES": "4"})])
+                                          ("sponza", 4, {"WGT_CNODE": "4"}), ("bunny", 1, {}),
+                                          ("bunny", 1, {"WGT_CNODE": "4"})])
 def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatch):
     """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
     oracle (OpenMP), through the default kernel of each scene: sponza on the 80-B compact
@@ -370,14 +369,6 @@ _SCHED_REF = {}
                                  {"WGT_CNODE": "4", "WGT_PS_WAVES": "5"},
                                  {"WGT_CNODE": "4", "WGT_PS_TO_TRAV": "1", "WGT_PS_TO_SERVICE": "63"},
                                  {"WGT_CNODE": "4", "WGT_TRI_RATIO": "1"}, {"WGT_CNODE": "4", "WGT_TRI_RATIO": "1000000"},
-                                 # two pixels per lane (round 5, k_render_ps2): both node forms, block order,
-                                 # second rays swapped in one lane at a time or only at the phase's end,
-                                 # every lane in every traversal phase, triangle steps at once
-                                 {"WGT_PS_WAVES": "4"}, {"WGT_PS_WAVES": "4", "WGT_CNODE": "1"},
-                                 {"WGT_PS_WAVES": "4", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "4", "WGT_PX2_SWAP": "1"},
-                                 {"WGT_PS_WAVES": "4", "WGT_PX2_SWAP": "64"},
-                                 {"WGT_PS_WAVES": "4", "WGT_PS_TO_TRAV": "1", "WGT_PS_TO_SERVICE": "63"},
-                                 {"WGT_PS_WAVES": "4", "WGT_PQ_REFILL": "64"}, {"WGT_PS_WAVES": "4", "WGT_TRI_RATIO": "1"},
                                  ])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the

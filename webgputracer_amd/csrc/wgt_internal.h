@@ -150,12 +150,6 @@ struct DevFrame {
   // of the lane (wave w, lane l) at ps_spill[e * ps_spill_stride + w * 64 + l] (launch_render)
   int* ps_spill;
   uint32_t ps_spill_stride;
-  // two pixels per lane (DevScene::ps_waves == 4, k_render_ps2): a traversal step swaps the
-  // lanes' ready second rays in once >= ps_px2_swap lanes have finished theirs
-  uint32_t ps_px2_swap;
-  // A/B forms at 4 waves per SIMD (WGT_PX2_MODE): 0 = two pixels per lane, 1 = k_render_ps2 with
-  // one pixel per lane (the second context never takes one), 2 = k_render_ps at 4 waves
-  uint32_t ps_px2_mode;
 };
 
 enum {

@@ -393,294 +393,6 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   }
 }
 
-// ---------------------------------------------------------------------------
-// Two pixels per lane (DevScene::ps_waves == 4, WGT_PS_WAVES=4).
-// k_render_ps's traversal phase runs at 0.45 of its lanes: a lane whose ray has finished idles
-// until the wave's next service pass.  Here a lane holds a second pixel whose next ray waits
-// ready (quad scan and trav_init done) in registers, and a traversal step swaps it in for a
-// finished ray, so a lane traverses up to two rays per phase.  The second pixel is never in the
-// middle of a traversal, so both share the lane's one LDS stack (4-byte entries: 4 waves per
-// SIMD hold 16 x 64 x 32 x 4 B = 128 KB).  A service pass serves both pixels with one copy of
-// the service code: the second is swapped into the active registers and back.  A ray starts
-// its traversal at the root, with scalar loads when it starts in a service pass and as an
-// ordinary node step when it is swapped in during a traversal phase: the same visit.  Every
-// pixel's result depends only on its coordinates and seed, whichever lane or context runs it.
-struct Px2 {
-  Pixel px;
-  uint32_t po;
-  f3 ro, rd, pc;
-  int depth;
-  f3 inv, ot;  // the ray's Trav (trav_init) and result; the active pixel keeps them in t
-  float bt;
-  uint32_t bi;
-  uint32_t q_prim;
-  float q_t;
-  uint32_t pblock, work;  // COST
-  bool have, trav, pending, fin, nanray;
-};
-template <class T>
-__device__ __forceinline__ void swp(T& x, T& y) {
-  const T z = x;
-  x = y;
-  y = z;
-}
-// exchange the active pixel (a, and the ray fields of t) with the second one; t's traversal
-// position (ref, open leaf, stack top) stays: it belongs to the lane's stack
-__device__ __forceinline__ void px2_swap(Px2& a, Trav& t, Px2& b) {
-  swp(a.px, b.px);
-  swp(a.po, b.po);
-  swp(a.ro, b.ro);
-  swp(a.rd, b.rd);
-  swp(a.pc, b.pc);
-  swp(a.depth, b.depth);
-  swp(t.inv, b.inv);
-  swp(t.ot, b.ot);
-  swp(t.bt, b.bt);
-  swp(t.bi, b.bi);
-  swp(a.q_prim, b.q_prim);
-  swp(a.q_t, b.q_t);
-  swp(a.pblock, b.pblock);
-  swp(a.work, b.work);
-  swp(a.have, b.have);
-  swp(a.trav, b.trav);
-  swp(a.pending, b.pending);
-  swp(a.fin, b.fin);
-  swp(a.nanray, b.nanray);
-}
-
-template <bool STATS, bool COST, int CN>
-__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4)))
-k_render_ps2(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
-             float4* __restrict__ out32, uint32_t* __restrict__ outhit,
-             unsigned long long* __restrict__ counters, uint32_t* __restrict__ queue) {
-  static_assert(CN == 0 || CN == 1, "two pixels per lane: the 128-B and 80-B node forms");
-  extern __shared__ int s_stack[];  // sc.stack 4-byte entries per lane, ps_stack_lds_bytes
-  Stack32 lds;
-  lds.p = s_stack + threadIdx.x;
-  const uint32_t lane = threadIdx.x;
-  const Light L{xyz(sc.quads[0]), xyz(sc.quads[1]), xyz(sc.quads[2])};
-  const uint32_t nsamp = fr.sqrt_spp * fr.sqrt_spp;
-  const uint32_t n_slots = fr.n_slots;
-  Px2 a{}, b{};
-  a.q_prim = b.q_prim = kNoHit;
-  a.q_t = b.q_t = kRayMax;
-  Trav t;
-  t.inv = t.ot = f3{0.0f, 0.0f, 0.0f};
-  t.bt = 0.0f;
-  t.bi = kNoHit;
-  t.ref = kNoRef;
-  t.lf = t.le = 0u;
-  t.sp = 0;
-  // t's traversal position belongs to the active pixel's ray (started implies a.trav); a ray
-  // made ready by a service pass has not started until its root step
-  bool started = false;
-  bool exhausted = false;  // the queue is empty for this lane
-  TravStats st{};
-  Counters c{0u, 0u, 0u, 0u, 0u, 0u};
-  uint64_t cyc_svc = 0, cyc_trav = 0;
-  // STATS (wgt_stats fields of the phase-split kernel's regions, reused here): cyc_refill = the
-  // waves' lifetimes, cyc_root = the longest, cyc_camera = service-loop iterations (per wave);
-  // stack_spills / stack_refills = second rays swapped in by traversal steps / service passes
-  const uint64_t t_start = STATS ? __builtin_amdgcn_s_memtime() : 0;
-  uint32_t svc_iters = 0;
-
-  for (;;) {
-    // ------------------------------------------------------------ service phase
-    uint64_t t_phase = STATS ? __builtin_amdgcn_s_memtime() : 0;
-    for (;;) {
-      // the active pixel, then the second one: one copy of the service code per context
-      auto serve = [&](Px2& x, f3& inv, f3& ot, float& bt, uint32_t& bi, bool refill_ok) __attribute__((always_inline)) {
-        if (x.fin) {  // a finished pixel: write it
-          if (COST) {
-            atomicAdd(fr.cost + x.pblock, x.work);
-            x.work = 0;
-          } else {
-            write_pixel(fr, x.po, x.px, out8, out32, outhit);
-          }
-          if (STATS) ++c.px;
-          x.fin = false;
-        }
-        // refill: lanes without a pixel in this context take consecutive slots, one atomic per wave
-        const unsigned long long idle = __ballot(!x.have && !exhausted);
-        if (idle != 0ull && refill_ok) {
-          const uint32_t n_idle = (uint32_t)__popcll(idle);
-          if (n_idle >= fr.pq_refill || __ballot(a.have || b.have) == 0ull) {
-            const int leader = __ffsll((long long)idle) - 1;
-            uint32_t base = 0;
-            if ((int)lane == leader) base = atomicAdd(queue, n_idle);
-            base = __shfl(base, leader);
-            if (!x.have && !exhausted) {
-              const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
-              if (slot >= n_slots) {
-                exhausted = true;
-              } else {
-                const bool quarter = COST && !fr.pq_lpt_all;
-                const uint32_t sb = quarter ? (slot >> 4) : (slot >> 6);
-                const uint32_t sl = quarter ? (((slot & 3u) << 1) | (((slot >> 2) & 3u) << 4)) : (slot & 63u);
-                const uint32_t blk = fr.perm ? fr.perm[sb] : sb;
-                if (slot_setup(fr, tiles, blk, sl, x.po, x.px)) {
-                  x.have = true;
-                  x.depth = 0;
-                  x.pblock = blk;
-                }
-              }
-            }
-          }
-        }
-        if (x.have && !x.trav) {
-          if (STATS) simt_count(c.lw, c.ll);
-          if (x.pending) {
-            // finalise: rebuild the quad hit, merge triangles, scan spheres, shade
-            Hit h;
-            if (x.nanray) {
-              nan_hit(sc, x.ro, x.rd, h);
-              if (STATS) { ++c.q; ++c.nan; }
-              x.nanray = false;
-            } else {
-              float4 pre[2];
-              preload_tshade(sc, bi, pre[0], pre[1]);
-              quad_rebuild(sc, x.ro, x.rd, x.q_prim, x.q_t, h);
-              finish_hit(sc, x.ro, x.rd, bt, bi, h, pre);
-              if (STATS) { ++c.q; ++c.tr; }
-            }
-            first_hit(x.px, x.depth, h.prim, x.po, outhit);
-            const bool end = shade(sc, L, h, x.depth, x.px.seed, x.ro, x.rd, x.pc);
-            ++x.depth;
-            if (end || x.depth == (COST ? (int)fr.pq_depth : kRayDepth)) {
-              end_sample(fr, x.px, x.pc);
-              x.depth = 0;
-            }
-            x.pending = false;
-          }
-          // the pixel's next ray, made ready (its root step waits until it is the active ray)
-          for (;;) {
-            if (px_done(fr, x.px)) {
-              x.have = false;
-              x.fin = true;
-              break;
-            }
-            if (x.depth == 0) {
-              camera_ray(fr, x.px, x.ro, x.rd);
-              x.pc = f3{1.0f, 1.0f, 1.0f};
-            }
-            if (has_nan(x.ro) || has_nan(x.rd)) {
-              if (!sc.last_sphere_emissive) {
-                first_hit(x.px, x.depth, last_prim(sc), x.po, outhit);
-                skip_nan_path<STATS>(sc, fr, x.px, x.depth, c);
-                x.depth = 0;
-                continue;
-              }
-              x.nanray = true;  // resolved and shaded at the next finalise
-              x.pending = true;
-              break;
-            }
-            Hit h;
-            quad_scan(sc, x.ro, x.rd, h, x.q_t);
-            x.q_prim = h.prim;
-            Trav ti;
-            trav_init<CN>(sc, x.ro, x.rd, x.q_prim != kNoHit, x.q_t, ti);
-            inv = ti.inv;
-            ot = ti.ot;
-            bt = ti.bt;
-            bi = ti.bi;
-            if (COST) x.work += fr.pq_svc_cost;
-            x.trav = true;
-            break;
-          }
-        }
-      };
-      serve(a, t.inv, t.ot, t.bt, t.bi, true);
-      serve(b, b.inv, b.ot, b.bt, b.bi, fr.ps_px2_mode != 1);
-      // a lane whose active pixel has no ray takes the second pixel's ready one, and the rays
-      // not started take their root step (a uniform address: scalar loads)
-      if (STATS) ++svc_iters;
-      if (!a.trav && b.trav) {
-        px2_swap(a, t, b);
-        if (STATS) st.refills++;
-      }
-      if (a.trav && !started) {
-        t.ref = 0;
-        t.lf = t.le = 0u;
-        t.sp = 0;
-        root_step<STATS, CN>(sc, t, lds, st);
-        if (trav_done(t)) {
-          a.trav = false;
-          a.pending = true;
-        } else {
-          started = true;
-        }
-      }
-      if ((uint32_t)__popcll(__ballot(a.trav)) >= fr.ps_to_trav) break;
-      const bool need = (a.have && !a.trav) || (b.have && !b.trav) || a.fin || b.fin;
-      if (!__any(need)) {
-        // lanes left without pixels while nothing traverses: refill again (a wave without
-        // pixels refills whatever the count)
-        if (__ballot((!a.have || !b.have) && !exhausted) != 0ull && __ballot(a.trav) == 0ull) continue;
-        break;
-      }
-    }
-    if (STATS) {
-      const uint64_t now = __builtin_amdgcn_s_memtime();
-      cyc_svc += now - t_phase;
-      t_phase = now;
-    }
-    if (__ballot(a.have || b.have || !exhausted) == 0ull) break;
-    // --------------------------------------------------------- traversal phase
-    uint32_t to_service = fr.ps_to_service;
-    if (fr.ps_svc_frac) {
-      const uint32_t live = (uint32_t)__popcll(__ballot(a.have || b.have));
-      const uint32_t sparse = (live * fr.ps_svc_frac) >> 6;
-      to_service = sparse < to_service ? sparse : to_service;
-    }
-    for (;;) {
-      const bool can_node = t.ref != kNoRef;
-      const bool can_tri = t.lf < t.le;
-      const uint32_t nn = (uint32_t)__popcll(__ballot(can_node));
-      const uint32_t nl = (uint32_t)__popcll(__ballot(can_tri));
-      const bool tri_mode = nn == 0 || nl * 100u >= nn * fr.tri_ratio;
-      if (STATS && (tri_mode ? can_tri : can_node)) simt_count(st.wave_steps, st.lane_steps);
-      if (COST && (tri_mode ? can_tri : can_node)) ++a.work;
-      if (tri_mode) {
-        if (can_tri) tri_step<STATS, CN>(sc, a.ro, a.rd, t, lds, st);
-      } else {
-        if (can_node) node_step<STATS, CN>(sc, t, lds, st);
-      }
-      if (a.trav && trav_done(t)) {
-        a.trav = false;
-        a.pending = true;
-        started = false;
-      }
-      uint32_t ntrav = (uint32_t)__popcll(__ballot(a.trav));
-      // swap the ready second rays in, in batches (a swap costs ~30 VALU for the wave)
-      const bool cand = !a.trav && b.trav;
-      const uint32_t nc = (uint32_t)__popcll(__ballot(cand));
-      if (nc != 0u && (nc >= fr.ps_px2_swap || ntrav <= to_service)) {
-        if (cand) {
-          px2_swap(a, t, b);
-          t.ref = 0;  // a finished traversal left no open leaf and an empty stack
-          started = true;
-          if (STATS) st.spills++;
-        }
-        ntrav += nc;
-      }
-      if (ntrav == 0) break;
-      if (ntrav <= to_service && __any(!a.trav && (a.have || b.have || !exhausted))) break;
-    }
-    if (STATS) cyc_trav += __builtin_amdgcn_s_memtime() - t_phase;
-  }
-  if (STATS) {
-    flush_counters(counters, c, st, nsamp);
-    if (lane == 0) {
-      atomicAdd(&counters[CNT_CYC_SERVICE], (unsigned long long)cyc_svc);
-      atomicAdd(&counters[CNT_CYC_TRAV], (unsigned long long)cyc_trav);
-      const uint64_t life = __builtin_amdgcn_s_memtime() - t_start;
-      atomicAdd(&counters[CNT_CYC_REFILL], (unsigned long long)life);
-      atomicMax(&counters[CNT_CYC_ROOT], (unsigned long long)life);
-      atomicAdd(&counters[CNT_CYC_CAMERA], (unsigned long long)svc_iters);
-    }
-  }
-}
-
 template <bool TRIS>
 __global__ void __launch_bounds__(kBlock)
 k_trace(DevScene sc, const float* __restrict__ rays, uint32_t n, uint32_t* __restrict__ prim,
@@ -831,12 +543,6 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
                uint32_t* queue) {
   if (sc.n_tris == 0) {
     k_render_ps<STATS, COST, 0, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
-  } else if (sc.ps_waves == 4 && f.ps_px2_mode == 2) {  // A/B: the phase-split kernel at 4 waves
-    if (cn) k_render_ps<STATS, COST, 1, 4, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
-    else k_render_ps<STATS, COST, 0, 4, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
-  } else if (sc.ps_waves == 4) {  // two pixels per lane (the 128-B or 80-B nodes)
-    if (cn) k_render_ps2<STATS, COST, 1><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
-    else k_render_ps2<STATS, COST, 0><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue);
   } else if (sc.ps_waves == 7) {  // parked state only (the whole stack does not fit LDS at 7)
     if (cn == 2) k_render_ps<STATS, COST, 2, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
     else if (cn == 1) k_render_ps<STATS, COST, 1, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
@@ -862,7 +568,7 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
 // 4 = the wide 8-slot records (when the scene has them and the traversal state is not parked).
 int node_form(const DevScene& sc, const DevFrame& fr) {
   const float cam = fmaxf(fmaxf(fabsf(fr.ox), fabsf(fr.oy)), fabsf(fr.oz));
-  if (fr.cnode == 4 && sc.w8 && !sc.ps_park && sc.ps_waves >= 5 && sc.ps_waves <= 6 && cam <= sc.cbound) return 3;
+  if (fr.cnode == 4 && sc.w8 && !sc.ps_park && sc.ps_waves <= 6 && cam <= sc.cbound) return 3;
   if (fr.cnode == 3 && sc.ps_waves >= 6 && cam <= sc.c64bound) return 2;
   if (!(cam <= sc.cbound)) return 0;
   return fr.cnode == 1 || fr.cnode == 3 ||
@@ -957,10 +663,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
 // k_render_ps<STATS = false, COST = false, CN, W> of a launchable form
 template <int W, bool PK>
 const void* ps_kernel(int cn) {
-  if constexpr (W == 4) {
-    return cn ? reinterpret_cast<const void*>(&k_render_ps2<false, false, 1>)
-              : reinterpret_cast<const void*>(&k_render_ps2<false, false, 0>);
-  } else if constexpr (W == 7) {
+  if constexpr (W == 7) {
     return cn == 2 ? reinterpret_cast<const void*>(&k_render_ps<false, false, 2, 7, true, true>)
                    : cn == 1 ? reinterpret_cast<const void*>(&k_render_ps<false, false, 1, 7, true, true>)
                              : reinterpret_cast<const void*>(&k_render_ps<false, false, 0, 7, true, true>);
@@ -985,10 +688,8 @@ hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
     per_cu = 1 << 30;
     for (int cn = 0; cn < 4; ++cn) {
       if (cn == 2 && !(sc.ps_waves >= 6 && sc.c64bound >= 0.0f)) continue;
-      if (cn == 3 && !(sc.w8 && !sc.ps_park && sc.ps_waves >= 5 && sc.ps_waves <= 6)) continue;
-      if (cn >= 2 && sc.ps_waves == 4) continue;
-      const void* k = sc.ps_waves == 4 ? ps_kernel<4, false>(cn)
-                      : sc.ps_waves == 7 ? ps_kernel<7, true>(cn)
+      if (cn == 3 && !(sc.w8 && !sc.ps_park && sc.ps_waves <= 6)) continue;
+      const void* k = sc.ps_waves == 7 ? ps_kernel<7, true>(cn)
                       : sc.ps_waves == 6 ? (sc.ps_park ? ps_kernel<6, true>(cn) : ps_kernel<6, false>(cn))
                                          : (sc.ps_park ? ps_kernel<5, true>(cn) : ps_kernel<5, false>(cn));
       int n = 0;

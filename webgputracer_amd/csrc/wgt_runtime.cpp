@@ -153,7 +153,6 @@ uint32_t ps_waves_for(const BvhOut& bvh, uint32_t n_tris) {
   if (n_tris == 0) return (uint32_t)kPsWavesNoTris;
   const uint32_t forced = env_u32("WGT_PS_WAVES", 0);
   if (forced == 5) return 5u;
-  if (forced == 4) return 4u;  // two pixels per lane (k_render_ps2, 4-byte entries)
   const bool fits24 = bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris;
   // 7 waves per SIMD (72 VGPRs) exist with the parked state only (WGT_PS_WAVES=7 parks)
   if (forced == 7 && fits24) return 7u;
@@ -180,7 +179,7 @@ bool c64_fits(const BvhOut& bvh) {
 // 7 waves per SIMD park (the only form of that budget); a WGT_PS_WAVES=7 request that the tree cannot
 // take (ps_waves_for gave 6 or 5) does not park unless WGT_PARK asks for it.
 void ps_park_cap(uint32_t n_tris, uint32_t stack, uint32_t waves, uint32_t& park, uint32_t& cap) {
-  park = n_tris > 0 && waves != 4 && (env_u32("WGT_PARK", 0) || waves == 7) ? 1u : 0u;
+  park = n_tris > 0 && (env_u32("WGT_PARK", 0) || waves == 7) ? 1u : 0u;
   cap = stack;
   if (!park) return;
   uint32_t c = std::min(stack, ps_cap_max(waves));
@@ -247,8 +246,6 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   // alone -0.6% against full paths, 3 rounds on one box (profiles/sweeps/r04_pq_depth.log)
   fr.pq_depth = std::min<uint32_t>(std::max<uint32_t>(env_u32("WGT_PQ_DEPTH", 6), 1u), (uint32_t)kRayDepth);
   fr.pq_lpt_all = env_u32("WGT_PQ_LPT_ALL", 1);  // sweep: all pixels -3% (sponza), -4% (bunny) at 256 spp
-  fr.ps_px2_swap = std::max<uint32_t>(env_u32("WGT_PX2_SWAP", 8), 1u);
-  fr.ps_px2_mode = env_u32("WGT_PX2_MODE", 0);
   return fr;
 }
 
