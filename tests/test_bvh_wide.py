@@ -159,12 +159,21 @@ def test_wide_full_size_meshes():
         assert avg > 4.0, f"{kind}: {avg:.2f} slots per node"
 
 
-def test_wide_env_off(monkeypatch):
-    monkeypatch.setenv("WGT_W8", "0")
-    from webgputracer_amd._lib import WgtError
-
-    with pytest.raises(WgtError):
-        w.bvh_build_wide(random_soup(100, 1))
+@pytest.mark.parametrize("w8,cnode,built", [(None, None, 0), (None, "4", 1), (None, "2", 0), ("1", None, 1),
+                                             ("0", "4", 0)])
+def test_wide_built_on_request(monkeypatch, w8, cnode, built):
+    """The wide form is opt-in at the build (host/bvh.cpp WideWanted): with WGT_CNODE=4 or WGT_W8=1,
+    never with WGT_W8=0; the explicit export (wgt_bvh_build_wide) builds it whatever the environment."""
+    for k, v in (("WGT_W8", w8), ("WGT_CNODE", cnode)):
+        if v is None:
+            monkeypatch.delenv(k, raising=False)
+        else:
+            monkeypatch.setenv(k, v)
+    tris = random_soup(100, 1)
+    info, _, _ = w.bvh_build(tris)
+    assert info["bvh_w8"] == built
+    winfo, recs, _ = w.bvh_build_wide(tris)
+    assert winfo["bvh_w8"] == 1 and len(recs) == winfo["w8_records"]
 
 
 # ---------------------------------------------------------------------------------------------

@@ -273,7 +273,8 @@ def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
     check_counters(g["stats"], r["counters"], oracle)
     info = ctx.scene_info()
     assert info["n_tris"] == len(T) and info["bvh_max_depth"] <= 94
-    assert info["bvh_compact"] == 1 and info["bvh_c64"] == 1 and info["bvh_w8"] == 1
+    # the wide form is built only when asked for at the upload (WGT_CNODE=4 or WGT_W8=1)
+    assert info["bvh_compact"] == 1 and info["bvh_c64"] == 1 and info["bvh_w8"] == (1 if cnode == "4" else 0)
     assert info["node_form"] == {"2": 1, "0": 0, "3": 2, "4": 3}[cnode]
 
 

@@ -630,10 +630,14 @@ float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes, double G, d
 // A visit pushes at most two stack entries whatever its width (the group of internal children it
 // does not descend into, and a second triangle group), so the stack bound is 2 x the depth: the
 // budget is the depth.  Like the BVH4 collapse it only regroups BVH2 boxes.
-// WGT_W8=0 skips the wide form (its own BVH2 build and collapse: about as long as the BVH4's)
+// The wide form is opt-in (only WGT_CNODE=4 reads it) and its own BVH2 build and collapse take about
+// as long as the BVH4's: built when WGT_W8=1, or with WGT_W8 unset when WGT_CNODE=4 at the build
+// (the scene upload); never with WGT_W8=0.  wgt_bvh_build_wide asks for it (BvhOut::want_wide).
 bool WideWanted() {
   const char* v = std::getenv("WGT_W8");
-  return !(v && *v && std::atoi(v) == 0);
+  if (v && *v) return std::atoi(v) != 0;
+  const char* c = std::getenv("WGT_CNODE");
+  return c && *c && std::atoi(c) == 4;
 }
 double W8NodeCost() {
   const char* v = std::getenv("WGT_W8_NODE");
@@ -919,6 +923,7 @@ bool BuildWide(const wgt_triangle* tris, std::vector<Prim> prims, uint32_t max_d
 
 bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
               uint32_t narrow_limit, double narrow_ratio, double origin_bound, BvhOut& out, std::string& err) {
+  const bool want_wide = out.want_wide || WideWanted();
   out = BvhOut{};
   if (n == 0) { err = "BuildBvh: no triangles"; return false; }
   // leaf walks use 32-bit byte offsets into the 64-B records (wgt_geom.h kTriRecordBytes)
@@ -942,7 +947,7 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
       }
     }
   }
-  if (WideWanted()) prims_in = prims;
+  if (want_wide) prims_in = prims;
   if (MedianDepth(n) > max_depth_limit) {
     err = "BuildBvh: too many triangles for depth limit " + std::to_string(max_depth_limit);
     return false;

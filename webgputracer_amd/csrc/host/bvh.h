@@ -27,6 +27,7 @@ struct BvhOut {
   uint32_t stack_need = 0;            // worst-case traversal stack entries (exact for this tree)
   // the wide form (wgt_geom.h kW8*): records 8g + s of 32 words, triangle records 4(8g + s) + i
   // of kTriRecordFloats, over its own BVH2 (leaves <= kW8LeafMax); w8_ok = false without it
+  bool want_wide = false;  // input: build the wide form whatever the environment (wgt_bvh_build_wide)
   bool w8_ok = false;
   std::vector<uint32_t> w8nodes;
   std::vector<float> w8tris;

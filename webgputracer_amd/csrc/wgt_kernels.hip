@@ -565,14 +565,15 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
 // 4 MB L2 (sponza stand-in: 7.3 MB -> 4.6 MB; default), 3 = 64-B (at 6 waves per SIMD, when
 // the tree fits the form; else as 1).  A tree that fits keeps the 128-B nodes, whose step
 // needs fewer VALU.
-// 4 = the wide 8-slot records (when the scene has them and the traversal state is not parked).
+// 4 = the wide 8-slot records (when the scene has them and the traversal state is not parked; else as
+// 2: the scene was uploaded without WGT_CNODE=4 or WGT_W8=1, host/bvh.cpp WideWanted).
 int node_form(const DevScene& sc, const DevFrame& fr) {
   const float cam = fmaxf(fmaxf(fabsf(fr.ox), fabsf(fr.oy)), fabsf(fr.oz));
   if (fr.cnode == 4 && sc.w8 && !sc.ps_park && sc.ps_waves <= 6 && cam <= sc.cbound) return 3;
   if (fr.cnode == 3 && sc.ps_waves >= 6 && cam <= sc.c64bound) return 2;
   if (!(cam <= sc.cbound)) return 0;
   return fr.cnode == 1 || fr.cnode == 3 ||
-                 (fr.cnode == 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes)
+                 ((fr.cnode == 2 || fr.cnode == 4) && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes)
              ? 1
              : 0;
 }

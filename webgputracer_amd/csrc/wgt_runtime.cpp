@@ -571,6 +571,7 @@ int wgt_bvh_build_wide(const wgt_triangle* tris, uint32_t n_tris, uint32_t* recs
                        float* tris_out, uint32_t tri_recs_cap, wgt_scene_info* info) {
   if (!tris || n_tris == 0 || !info) return fail(nullptr, WGT_E_INVALID, "null triangles or info");
   BvhOut bvh;
+  bvh.want_wide = true;
   std::string err;
   if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(),
                 kOriginBoundScale * scene_extent(nullptr, 0, nullptr, 0, tris, n_tris), bvh, err))
