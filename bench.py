@@ -534,7 +534,12 @@ def main():
             "roofline": {"bound": limiter(hbm_frac, sq), "achieved": round(survey_bytes / (kern_ms * 1e-3) / 1e9, 2) if kern_ms > 0
                          else 0.0, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(survey_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 5) if kern_ms > 0
-                         else 0.0, "traffic": traffic, "traffic_build_id": tj_id if traffic is not None else None,
+                         else 0.0,
+                         # the same bytes over one launch alone on an idle device (its ramp-up and drain
+                         # included, no overlap with a neighbouring frame): the per-dispatch figure
+                         "frac_isolated": round(survey_bytes / (iso * 1e-3) / 1e9 / HBM_PEAK_GBS, 5)
+                         if iso else None,
+                         "traffic": traffic, "traffic_build_id": tj_id if traffic is not None else None,
                          "traffic_source": traffic_source, "traffic_note": traffic_note,
                          # measured HBM traffic / launch time / peak: the DRAM side of the roofline
                          "hbm_frac": hbm_frac, "write_bytes_per_launch": write_b,

@@ -302,6 +302,9 @@ def test_bench_line_contract(tmp_path):
     rf = line["roofline"]
     assert rf["unit"] == "GB/s" and rf["peak"] > 0
     assert abs(rf["frac"] - rf["achieved"] / rf["peak"]) < 1e-3
+    # the same algorithmic bytes over one launch alone (pipeline 2: a launch on an idle device)
+    iso = line["timing"]["isolated_launch_ms"]
+    assert abs(rf["frac_isolated"] - rf["frac"] * line["kernel_ms"] / iso) < 1e-3
     # what bounds the kernel, from the run's own measurements (bench.limiter): the measured HBM
     # traffic's share of the peak, the VALU-busy fraction and the wave-cycle split
     assert abs(rf["hbm_frac"] - rf["traffic"] / (line["kernel_ms"] * 1e-3) / 1e9 / rf["peak"]) < 1e-3
