@@ -15,11 +15,14 @@ value = closest-hit queries actually traced (non-NaN rays, counted on the device
 an instrumented pass over the same tiles) summed over ranks x steps / max-over-ranks
 wall time of the K timed steps.  Scene/BVH upload and tile lists are resident in HBM
 before timing.  Each render call is launched on its step's stream, where HIP events
-bracket it; with frames in flight the per-launch time (roofline.achieved) is the
-interval between consecutive launch completions (a launch's own event pair would also
-count the time it waits for the previous frame's CUs), with --pipeline 1 the event pair:
-the 1-spp cost pre-pass + LPT ordering (~1 % of the call at 256 spp) and the main kernel
-k_render_ps (the rocprof kernel trace under profiles/ lists them separately).
+bracket it; with frames in flight the per-launch time (roofline.achieved) is the span
+from the first timed launch's start to the last one's end divided by K (a launch's own
+event pair would also count the time it waits for the previous frame's CUs), with
+--pipeline 1 the mean event pair: the 1-spp cost pre-pass + LPT ordering (~1 % of the
+call at 256 spp) and the main kernel k_render_ps (the rocprof kernel trace under
+profiles/ lists them separately).  At N > 1 every rank reports the same figures for its
+own tiles (per_rank: launch ms, gather ms, roofline frac), rank 0 times the CPU baseline
+and runs the live PMC passes on its own GPU (a frame of the per-GPU workload alone).
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--scene sponza|bunny|cornell]
   torchrun --nproc-per-node N bench.py --gpus N ...
@@ -44,8 +47,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s)
 # 64-B node + its 16-B ref record; a triangle test all 4 x 16 B of its 64-B record
 # (the padded box with the Moller-Trumbore inputs), a traced
 # ray 32 B of per-triangle shading data
-NODE_BYTES, CNODE_BYTES, C64NODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 64, 64, 32
-W8NODE_BYTES = 128  # a wide 8-slot record (round 5): one whole 128-B line per visit
+NODE_BYTES, CNODE_BYTES, TRI_BYTES, SHADE_BYTES = 112, 80, 64, 32
 # SURVEY §8(d)'s format-independent figure: 32 B per BVH node visit, 48 B per triangle
 # test, 32 B of shading record per traced ray (the same at any node encoding)
 SURVEY_NODE_BYTES, SURVEY_TRI_BYTES = 32, 48
@@ -54,26 +56,18 @@ L2_CALIB_JSON = os.path.join(ROOT, "profiles", "l2_calibration.json")
 
 
 def dominant_kernel(form: int, waves: int, tris: bool = True, park: bool = True) -> str:
-    """The timed k_render_ps instantiation <STATS, COST, node form (0 = 128-B, 1 = 80-B compact,
-    2 = 64-B compact, 3 = wide), waves per SIMD, triangles, parked traversal state> (a scene without
-    triangles runs the 8-wave instantiation without traversal)."""
+    """The timed k_render_ps instantiation <STATS, COST, node form (0 = 128-B, 1 = 80-B compact),
+    waves per SIMD, triangles, parked traversal state> (a scene without triangles runs the 8-wave
+    instantiation without traversal)."""
     if not tris:
         return "wgt::k_render_ps<false, false, 0, 8, false, false>"
     return f"wgt::k_render_ps<false, false, {int(form)}, {waves}, true, {'true' if park else 'false'}>"
 
 
 def node_form(info) -> int:
-    """The node form k_render_ps reads (wgt_kernels.hip node_form): 0 = 128-B, 1 = 80-B compact,
-    2 = 64-B compact, 3 = wide 8-slot records.  The library reports it for the reference camera
-    (scene_info node_form, round 5); an older build (A/B runs) is mirrored from WGT_CNODE: 0 = 128-B,
-    1 = 80-B compact, 2 = 80-B compact when the 128-B tree exceeds 4 MB, 3 = 64-B compact where the
-    tree fits it (scene_info bvh_c64), else 80-B."""
-    if "node_form" in info and info.get("bvh_w8", 0) in (0, 1) and info["node_form"] in (0, 1, 2, 3):
-        return int(info["node_form"])
-    mode = os.environ.get("WGT_CNODE", "2") or "2"
-    if mode == "3":
-        return 2 if info.get("bvh_c64", 0) and info.get("ps_waves") == 6 else 1
-    return 1 if mode == "1" or (mode == "2" and bool(info.get("bvh_compact", 0))) else 0
+    """The node form k_render_ps reads for the reference camera (wgt_kernels.hip node_form, reported
+    by the library as scene_info node_form): 0 = 128-B nodes, 1 = 80-B compact records."""
+    return int(info["node_form"])
 
 
 def parse():
@@ -156,13 +150,14 @@ def limiter(hbm_frac, sq):
     return "latency"
 
 
-def live_pmc(args, kernel, grid_waves=None):
+def live_pmc(args, kernel, grid_waves=None, local=0):
     """HBM bytes and L2 requests per launch of `kernel`, measured now on this device and binary:
     one rocprofv3 --pmc pass per counter group (never combined with traces; each pass within the
     per-block counter limits, under its own kill timeout) over a child run of this script that
     renders one frame of the same workload alone.  HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x
     1 KiB (FETCH_SIZE counts half the bytes of 16-B-per-lane reads on gfx950, MI355X_MICROARCH.md
-    §HBM).  Returns (result dict, note); the dict is None when a pass fails."""
+    §HBM).  At N > 1 the child runs on this rank's GPU (`local`) as a one-rank job.  Returns
+    (result dict, note); the dict is None when a pass fails."""
     import csv
     import shutil
     import subprocess
@@ -175,6 +170,7 @@ def live_pmc(args, kernel, grid_waves=None):
              "--height", str(args.height), "--spp", str(args.spp), "--tile", str(args.tile), "--steps", "1",
              "--warmup", "0", "--pipeline", "1", "--no-cpu-baseline", "--check", "off", "--pmc", "off",
              "--stats-reps", "1"]
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK=str(local), LOCAL_WORLD_SIZE="1")
     agg, calls = {}, 0
     t_end = time.monotonic() + PMC_BUDGET_S
     for ctrs in PMC_PASSES:
@@ -188,7 +184,7 @@ def live_pmc(args, kernel, grid_waves=None):
         cmd = ["timeout", "-s", "KILL", str(left), prof, "--pmc", *ctrs, "-d", d, "-o", "run", "--output-format",
                "csv", "--", *child]
         try:
-            r = subprocess.run(cmd, capture_output=True, text=True, timeout=left + 30, cwd=ROOT)
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=left + 30, cwd=ROOT, env=env)
             rows = []
             for root, _, files in os.walk(d):
                 for fn in files:
@@ -238,7 +234,7 @@ def cpu_baseline(args, scene, rank, world):
     """The oracle (CPU port, OpenMP) on a bounded row sample of the same workload,
     timed with its x86-64-v3 build (oracle/Makefile: liboracle_v3.so), which is first
     checked bit for bit against the reference build liboracle.so on a small tile."""
-    if rank != 0 or world != 1 or args.no_cpu_baseline:
+    if rank != 0 or args.no_cpu_baseline:
         return None
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle as po
@@ -432,7 +428,7 @@ def main():
         form = node_form(info)
         kernel = dominant_kernel(form, int(info.get("ps_waves", 5)), info["n_tris"] > 0,
                                  bool(info.get("ps_park", 0)))
-        node_b = (NODE_BYTES, CNODE_BYTES, C64NODE_BYTES, W8NODE_BYTES)[form]
+        node_b = (NODE_BYTES, CNODE_BYTES)[form]
         bytes_launch = (mine[4] * node_b + mine[5] * TRI_BYTES + mine[1] * SHADE_BYTES)
         achieved = bytes_launch / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
         survey_bytes = mine[4] * SURVEY_NODE_BYTES + mine[5] * SURVEY_TRI_BYTES + mine[1] * SHADE_BYTES
@@ -470,12 +466,14 @@ def main():
             pass
         # live PMC passes of this binary on this device (N = 1), in place of the profile entry
         traffic_source = "profile" if traffic is not None else None
-        if world == 1 and (args.pmc == "on" or (args.pmc == "auto" and args.steps > 0)):
+        if args.pmc == "on" or (args.pmc == "auto" and args.steps > 0):
             # the child renders one whole W x H frame at N = 1: its persistent grid is the device's
             # resident capacity or one wave per 8x8 pixel block, whichever is smaller
             res = int(info.get("ps_resident", 0))
             grid = min(((W + 7) // 8) * ((H + 7) // 8), res) if res else None
-            live, note = live_pmc(args, kernel, grid)
+            live, note = live_pmc(args, kernel, grid, local)
+            if live is not None and world > 1:
+                note += f" (rank 0's GPU, after the {world}-rank timed region)"
             if live is not None:
                 traffic, tj_id, traffic_note, traffic_source = live["hbm_bytes_per_launch"], build_id, note, "live"
                 sq, write_b = live["sq"], live["write_bytes_per_launch"]
@@ -526,8 +524,7 @@ def main():
             "simt_utilisation": {k: round(v, 4) for k, v in simt.items()},
             "per_launch": {"traced_rays": int(mine[1]), "node_visits": int(mine[4]), "tri_tests": int(mine[5]),
                            "algorithmic_bytes": int(survey_bytes), "loaded_bytes": int(bytes_launch),
-                           "kernel": kernel, "bvh_nodes": ("128 B", "compact 80-B records", "compact 64-B records",
-                                                                     "wide 8-slot 128-B records")[form]},
+                           "kernel": kernel, "bvh_nodes": ("128 B", "compact 80-B records")[form]},
             # achieved = SURVEY 8(d)'s algorithmic bytes (32 B per node visit, 48 B per triangle test, 32 B
             # per traced ray: independent of the node encoding) / the launch time.  The roofline priced is
             # HBM's; `bound` is what the measurements show bounds the kernel (limiter())
@@ -567,8 +564,14 @@ def main():
         }
         if world > 1:
             # where a multi-GPU step's time goes: each rank's launch time and its gather (which
-            # waits for the slowest rank's tiles), per step
-            line["per_rank"] = {"kernel_ms": [round(float(x), 3) for x in allv[:, 6]],
+            # waits for the slowest rank's tiles), per step; and each rank's roofline fraction from
+            # its own counts (SURVEY 8(d) bytes of its tiles) over its own launch time
+            rk_bytes = allv[:, 4] * SURVEY_NODE_BYTES + allv[:, 5] * SURVEY_TRI_BYTES + allv[:, 1] * SHADE_BYTES
+            rk_frac = [round(float(b / (t * 1e-3) / 1e9 / HBM_PEAK_GBS), 5) if t > 0 else 0.0
+                       for b, t in zip(rk_bytes, allv[:, 6])]
+            line["per_rank"] = {"roofline_frac": rk_frac,
+                                "traced_rays": [int(x) for x in allv[:, 1]],
+                                "algorithmic_bytes": [int(x) for x in rk_bytes],"kernel_ms": [round(float(x), 3) for x in allv[:, 6]],
                                 "gather_ms": [round(float(x), 3) for x in allv[:, 7]],
                                 "isolated_launch_ms": [round(float(x), 3) for x in allv[:, 8]],
                                 "kernel_ms_min_max": [round(float(allv[:, 6].min()), 3),

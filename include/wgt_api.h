@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define WGT_API_VERSION 1
+#define WGT_API_VERSION 2  /* 2: the 64-B and wide node forms removed (scene info fields) */
 
 enum {
   WGT_OK = 0,
@@ -122,12 +122,15 @@ typedef struct {
    * NaN handling, quad scan, root-node test */
   uint64_t cyc_refill, cyc_finalise, cyc_shade, cyc_camera, cyc_quads, cyc_root;
   /* persistent kernel with parked traversal state: LDS stack overflows moved to the
-   * lane's global stack, and refills from it; with the wide form
-   * (WGT_CNODE=4): second triangle groups pushed, and taken back (§4.2 item 23) */
+   * lane's global stack, and refills from it */
   uint64_t stack_spills, stack_refills;
   /* ... and traversals ended on the global stack's overflow exit (a wrong pixel; never taken:
    * the global stack holds the builder's bound, and the parity tests assert 0) */
   uint64_t stack_overflows;
+  /* traversal phase by BVH level: lane visits of nodes at levels 1-2 (the root is
+   * tested in the service phase), wave cycles of node steps, of the node steps whose visiting lanes
+   * are all at levels 1-2 (what an LDS copy of the top levels could shorten), and of triangle steps */
+  uint64_t top_node_visits, cyc_node_steps, cyc_top_steps, cyc_tri_steps;
 } wgt_stats;
 
 typedef struct {
@@ -146,17 +149,8 @@ typedef struct {
   uint32_t ps_park;       /* 1: the persistent kernel parks its traversal state in LDS during
                            * service passes */
   uint32_t ps_stack;      /* stack entries per lane it keeps in LDS (the rest: a global stack) */
-  uint32_t bvh_c64;       /* 1: the tree also has the 64-B compact form (WGT_CNODE=3) */
-  /* the wide form (8-slot 128-B records over its own BVH2, WGT_CNODE=4) */
-  uint32_t bvh_w8;        /* 1: the persistent kernel can read it */
-  uint32_t w8_groups, w8_nodes, w8_leaves, w8_depth;
-  uint32_t w8_stack;      /* its worst-case stack entries per lane: 2 x w8_depth */
-  float w8_step;          /* its decode step */
-  double w8_sah;          /* its SAH cost (node visit = triangle test = 1) */
-  uint32_t w8_records;    /* wgt_bvh_build_wide: record positions (8 per group + the root's 8) */
-  float w8_bound;         /* wgt_bvh_build_wide: the codes hold for ray origins within this bound */
   uint32_t node_form;     /* node form of the persistent kernel for the reference camera: 0 = 128-B,
-                           * 1 = 80-B compact, 2 = 64-B compact, 3 = wide (WGT_CNODE) */
+                           * 1 = 80-B compact (WGT_CNODE) */
   uint32_t ps_resident;   /* waves of the persistent grid (the device's resident capacity) */
 } wgt_scene_info;
 
@@ -193,11 +187,6 @@ int wgt_bvh_build(const wgt_triangle *tris, uint32_t n_tris, float *nodes_out, u
  * step.  Both outputs are required; nodes_cap must be >= bvh_nodes. */
 int wgt_bvh_build_compact(const wgt_triangle *tris, uint32_t n_tris, uint32_t *cnodes_out,
                           int32_t *crefs_out, uint32_t nodes_cap, float *step_out);
-/* Host only: the wide form of the same scene (wgt_geom.h kW8*): recs_out gets w8_records x 32
- * words (record 8g + s), tris_out its triangle records, 4 per record position, 16 floats each
- * (recs_cap / tri_recs_cap in records).  Call with NULL outputs to size them (info->w8_records). */
-int wgt_bvh_build_wide(const wgt_triangle *tris, uint32_t n_tris, uint32_t *recs_out, uint32_t recs_cap,
-                       float *tris_out, uint32_t tri_recs_cap, wgt_scene_info *info);
 
 /* ---- rendering (replaces the compute pass of Renderer::OnRender) --------- */
 /* Synchronous: render the rectangle [x0,x0+tw) x [y0,y0+th) of a W x H frame

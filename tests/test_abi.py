@@ -44,7 +44,8 @@ def test_struct_sizes_match_reference_layouts(wgt):
     assert _lib.SPHERE_DTYPE.itemsize == 32    # scene.h:47 sphere_stride_
     assert _lib.TRI_DTYPE.itemsize == 80       # scene.h:45 tri_stride_
     assert _lib.CAMERA_DTYPE.itemsize == 48    # camera.h:19-31
-    assert ctypes.sizeof(_lib.WgtStats) == 192  # + stack_spills, stack_refills (round 4), stack_overflows (5)
+    # + stack_spills, stack_refills (round 4), stack_overflows (5), the four by-level traversal figures (6)
+    assert ctypes.sizeof(_lib.WgtStats) == 224
 
 
 def test_ctypes_structs_match_the_header(tmp_path):
@@ -75,7 +76,9 @@ def test_ctypes_structs_match_the_header(tmp_path):
 def test_version(wgt):
     from webgputracer_amd import _lib
 
-    assert _lib.lib().wgt_version() == 1
+    # 2 since round 6 (the 64-B and wide node forms' scene-info fields removed); the wrapper refuses
+    # a library of another version (its structs mirror this header)
+    assert _lib.lib().wgt_version() == _lib.API_VERSION == 2
 
 
 def test_build_id_names_the_kernel_sources(wgt):

@@ -54,16 +54,10 @@ def test_dominant_kernel_names():
     arguments <STATS, COST, CN, W, TRIS, PK>)."""
     assert bench.dominant_kernel(1, 6) == "wgt::k_render_ps<false, false, 1, 6, true, true>"
     assert bench.dominant_kernel(0, 5, park=False) == "wgt::k_render_ps<false, false, 0, 5, true, false>"
-    assert bench.dominant_kernel(2, 6) == "wgt::k_render_ps<false, false, 2, 6, true, true>"
     assert bench.dominant_kernel(1, 6, tris=False) == "wgt::k_render_ps<false, false, 0, 8, false, false>"
 
 
-def test_node_form_from_env(monkeypatch):
-    info = {"bvh_compact": 1, "bvh_c64": 1, "ps_waves": 6}
-    for mode, form in (("0", 0), ("1", 1), ("2", 1), ("3", 2)):
-        monkeypatch.setenv("WGT_CNODE", mode)
-        assert bench.node_form(info) == form
-    monkeypatch.setenv("WGT_CNODE", "2")
-    assert bench.node_form({"bvh_compact": 0, "ps_waves": 6}) == 0
-    monkeypatch.setenv("WGT_CNODE", "3")
-    assert bench.node_form({"bvh_compact": 0, "bvh_c64": 0, "ps_waves": 6}) == 1
+def test_node_form_from_scene_info():
+    """The node form comes from the library's scene_info (0 = 128-B nodes, 1 = 80-B compact)."""
+    assert bench.node_form({"node_form": 1, "ps_waves": 6}) == 1
+    assert bench.node_form({"node_form": 0, "ps_waves": 5}) == 0

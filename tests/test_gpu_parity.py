@@ -258,11 +258,10 @@ def _sponza(wgt, oracle):
     return _SPONZA["scene"]
 
 
-@pytest.mark.parametrize("cnode", ["2", "0", "3", "4"])
+@pytest.mark.parametrize("cnode", ["2", "0", "1"])
 def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
     """Sponza stand-in: by default (2) the persistent kernel reads the 80-B compact records
-    (the 128-B tree exceeds one XCD's L2), 0 forces the 128-B nodes, 3 the 64-B compact
-    records, 4 the wide 8-slot records."""
+    (the 128-B tree exceeds one XCD's L2), 0 forces the 128-B nodes, 1 the compact records."""
     monkeypatch.setenv("WGT_CNODE", cnode)
     L, Q, S, T = _sponza(wgt, oracle)
     ctx.upload_scene(L, Q, S, T)
@@ -273,24 +272,22 @@ def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
     check_counters(g["stats"], r["counters"], oracle)
     info = ctx.scene_info()
     assert info["n_tris"] == len(T) and info["bvh_max_depth"] <= 94
-    # the wide form is built only when asked for at the upload (WGT_CNODE=4 or WGT_W8=1)
-    assert info["bvh_compact"] == 1 and info["bvh_c64"] == 1 and info["bvh_w8"] == (1 if cnode == "4" else 0)
-    assert info["node_form"] == {"2": 1, "0": 0, "3": 2, "4": 3}[cnode]
+    assert info["bvh_compact"] == 1
+    assert info["node_form"] == {"2": 1, "0": 0, "1": 1}[cnode]
 
 
 _FULL = {}
 
 
-@pytest.mark.parametrize("kind,spp,env", [("sponza", 4, {}), ("sponza", 4, {"WGT_CNODE": "3"}),
-                                          ("sponza", 4, {"WGT_PARK": "1"}), ("sponza", 4, {"WGT_PS_WAVES": "7"}),
-                                          ("sponza", 4, {"WGT_CNODE": "4"}), ("bunny", 1, {}),
-                                          ("bunny", 1, {"WGT_CNODE": "4"})])
+@pytest.mark.parametrize("kind,spp,env", [("sponza", 4, {}), ("sponza", 4, {"WGT_CNODE": "0"}),
+                                          ("sponza", 4, {"WGT_PARK": "1"}), ("bunny", 1, {}),
+                                          ("bunny", 1, {"WGT_CNODE": "1"})])
 def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatch):
     """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
     oracle (OpenMP), through the default kernel of each scene: sponza on the 80-B compact
-    records, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries; and
-    sponza on the 64-B compact records (WGT_CNODE=3), with parked traversal state (WGT_PARK=1,
-    an 18-entry LDS stack) and at 7 waves/SIMD (WGT_PS_WAVES=7, parked, 13 entries)."""
+    records, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries; and each
+    on the other node form, and sponza with parked traversal state (WGT_PARK=1, an 18-entry LDS
+    stack)."""
     for k, v in env.items():
         monkeypatch.setenv(k, v)
     L, Q, S, T = wgt.mesh_scene(kind)
@@ -357,19 +354,10 @@ _SCHED_REF = {}
                                  {"WGT_PARK": "1", "WGT_PS_CAP": "8"}, {"WGT_PARK": "1", "WGT_PS_CAP": "8", "WGT_CNODE": "1"},
                                  {"WGT_PARK": "1", "WGT_PS_CAP": "8", "WGT_PS_WAVES": "5"},
                                  {"WGT_PARK": "1", "WGT_PS_CAP": "9", "WGT_PQ_LPT": "0"},
-                                 # the 64-B compact records (runtime-selected since round 4)
-                                 {"WGT_CNODE": "3"}, {"WGT_CNODE": "3", "WGT_PARK": "1", "WGT_PS_CAP": "8"},
-                                 # 7 waves per SIMD (parked state only)
-                                 {"WGT_PS_WAVES": "7"}, {"WGT_PS_WAVES": "7", "WGT_CNODE": "1"},
-                                 {"WGT_PS_WAVES": "7", "WGT_CNODE": "3", "WGT_PS_CAP": "8"},
-                                 # the wide 8-slot records (round 5): 3-byte and (5 waves) 4-byte group
-                                 # entries, block order, every lane in every traversal phase, triangle
-                                 # steps as soon as one lane has a group open (1) or node steps while any
-                                 # lane has a node (the most second triangle groups pushed)
-                                 {"WGT_CNODE": "4"}, {"WGT_CNODE": "4", "WGT_PQ_LPT": "0"},
-                                 {"WGT_CNODE": "4", "WGT_PS_WAVES": "5"},
-                                 {"WGT_CNODE": "4", "WGT_PS_TO_TRAV": "1", "WGT_PS_TO_SERVICE": "63"},
-                                 {"WGT_CNODE": "4", "WGT_TRI_RATIO": "1"}, {"WGT_CNODE": "4", "WGT_TRI_RATIO": "1000000"},
+                                 # triangle steps as soon as one lane has a leaf open (1), or node steps
+                                 # while any lane has a node (the most second leaves parked on the stack)
+                                 {"WGT_TRI_RATIO": "1"}, {"WGT_TRI_RATIO": "1000000"},
+                                 {"WGT_TRI_RATIO": "1", "WGT_CNODE": "1"},
                                  ])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the
@@ -397,7 +385,7 @@ def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     check_counters(g["stats"], r["counters"], oracle)
 
 
-@pytest.mark.parametrize("cap,cnode", [("8", "2"), ("8", "1"), ("8", "3"), ("11", "2")])
+@pytest.mark.parametrize("cap,cnode", [("8", "2"), ("8", "1"), ("11", "2")])
 def test_stack_overflow_spill_and_refill(ctx, wgt, oracle, bunny, cap, cnode, monkeypatch):
     """The parked kernel's LDS stack bounded at 8 (or 11) entries (WGT_PS_CAP; the builder's
     bound is 31, a node step may start only from a top <= 4 = 8 - 4, the 4-entry bound

@@ -279,6 +279,46 @@ def test_bench_two_ranks_self_checks(tmp_path):
     assert pr["gather_ms_min_max"] == [min(pr["gather_ms"]), max(pr["gather_ms"])]
 
 
+def test_bench_four_ranks_full_line(tmp_path):
+    """bench.py at N = 4 (torch.distributed.run, gloo, all ranks on cuda:0) at 1080p with a reduced
+    spp: the line the driver's scaling run reads carries every field of the N = 1 line — the
+    self-check (check_frames_bit_exact), the roofline with traffic from rank 0's live rocprofv3
+    --pmc passes, the CPU baseline timed once on rank 0 — plus per_rank: each rank's launch and
+    gather times and its own roofline fraction from its own counts (reference analogue: the
+    multi-machine launcher, settings/run.py:10-24)."""
+    import json
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "4",
+           "--dist-backend", "gloo", "--scene", "bunny", "--spp", "4", "--steps", "2", "--warmup", "1",
+           "--cpu-rows", "2", "--stats-reps", "1", "--pmc", "on"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    line = json.loads(lines[0])
+    (tmp_path / "n4.json").write_text(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline", "build_id", "per_rank"):
+        assert k in line, k
+    assert line["n_gpus"] == 4 and line["check_frames_bit_exact"] is True and line["check"]["frames"] == 4
+    assert line["config"]["workload"] == "bunny-1920x1080-4spp"
+    rf = line["roofline"]
+    assert rf["traffic_source"] == "live" and rf["traffic"] > 0 and rf["traffic_build_id"] == line["build_id"]
+    assert rf["valu_busy"] is not None and rf["bound"] in ("hbm", "valu", "latency")
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port" and cb["sample"]
+    pr = line["per_rank"]
+    for k in ("kernel_ms", "gather_ms", "isolated_launch_ms", "roofline_frac", "traced_rays", "algorithmic_bytes"):
+        assert len(pr[k]) == 4, k
+    # rank 0's own fraction is the line's (the same bytes over the same launch time)
+    assert abs(pr["roofline_frac"][0] - rf["frac"]) <= 1e-4 * max(rf["frac"], 1e-9) + 1e-5
+    assert all(f > 0 for f in pr["roofline_frac"]) and all(t > 0 for t in pr["traced_rays"])
+    # weak scaling: the ranks' rays sum to the value's numerator
+    assert sum(pr["traced_rays"]) * line["steps"] / (line["ms_per_step"] * line["steps"] * 1e-3) / 1e6 == \
+        pytest.approx(line["value"], rel=2e-3)
+
+
 def test_bench_line_contract(tmp_path):
     """bench.py at N = 1 on a small workload prints one JSON line with every field of the driver's
     contract: throughput, timing, roofline (bound, achieved, peak, frac, traffic measured by the

@@ -26,6 +26,7 @@ TILE_DTYPE = np.dtype([("x0", "<u4"), ("y0", "<u4"), ("seed", "<u4"), ("frame", 
 assert QUAD_DTYPE.itemsize == 96 and SPHERE_DTYPE.itemsize == 32
 assert TRI_DTYPE.itemsize == 80 and CAMERA_DTYPE.itemsize == 48 and TILE_DTYPE.itemsize == 16
 
+API_VERSION = 2  # WGT_API_VERSION of include/wgt_api.h
 WGT_OK, WGT_E_INVALID, WGT_E_HIP, WGT_E_NOSCENE, WGT_E_IO, WGT_E_NOMEM = 0, -1, -2, -3, -4, -5
 NO_HIT = 0xFFFFFFFF
 
@@ -41,7 +42,9 @@ class WgtStats(ctypes.Structure):
                 ("cyc_refill", ctypes.c_uint64), ("cyc_finalise", ctypes.c_uint64),
                 ("cyc_shade", ctypes.c_uint64), ("cyc_camera", ctypes.c_uint64), ("cyc_quads", ctypes.c_uint64),
                 ("cyc_root", ctypes.c_uint64), ("stack_spills", ctypes.c_uint64),
-                ("stack_refills", ctypes.c_uint64), ("stack_overflows", ctypes.c_uint64)]
+                ("stack_refills", ctypes.c_uint64), ("stack_overflows", ctypes.c_uint64),
+                ("top_node_visits", ctypes.c_uint64), ("cyc_node_steps", ctypes.c_uint64),
+                ("cyc_top_steps", ctypes.c_uint64), ("cyc_tri_steps", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -54,11 +57,7 @@ class WgtSceneInfo(ctypes.Structure):
                 ("device_bytes", ctypes.c_uint64), ("sah_cost", ctypes.c_double), ("bvh_width", ctypes.c_uint32),
                 ("bvh_stack", ctypes.c_uint32), ("bvh2_nodes", ctypes.c_uint32), ("bvh2_depth", ctypes.c_uint32),
                 ("bvh_compact", ctypes.c_uint32), ("bvh_compact_step", ctypes.c_float), ("ps_waves", ctypes.c_uint32),
-                ("ps_park", ctypes.c_uint32), ("ps_stack", ctypes.c_uint32), ("bvh_c64", ctypes.c_uint32),
-                ("bvh_w8", ctypes.c_uint32), ("w8_groups", ctypes.c_uint32), ("w8_nodes", ctypes.c_uint32),
-                ("w8_leaves", ctypes.c_uint32), ("w8_depth", ctypes.c_uint32), ("w8_stack", ctypes.c_uint32),
-                ("w8_step", ctypes.c_float), ("w8_sah", ctypes.c_double), ("w8_records", ctypes.c_uint32),
-                ("w8_bound", ctypes.c_float), ("node_form", ctypes.c_uint32),
+                ("ps_park", ctypes.c_uint32), ("ps_stack", ctypes.c_uint32), ("node_form", ctypes.c_uint32),
                 ("ps_resident", ctypes.c_uint32)]
 
     def as_dict(self):
@@ -72,7 +71,7 @@ EXPORTS = [
     "wgt_render_tiles_stats", "wgt_render_tiles_profile", "wgt_trace_rays", "wgt_trace_rays_async", "wgt_sync", "wgt_selftest_math", "wgt_stream",
     "wgt_pipeline_stream",
     "wgt_scene_cornell", "wgt_make_triangles", "wgt_load_obj", "wgt_procedural_mesh",
-    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build", "wgt_bvh_build_compact", "wgt_bvh_build_wide",
+    "wgt_write_obj", "wgt_write_png", "wgt_bvh_build", "wgt_bvh_build_compact",
     "wgt_render_frames",
 ]
 
@@ -129,7 +128,6 @@ def lib():
         "wgt_write_obj": (I, [ctypes.c_char_p, P, U32]),
         "wgt_write_png": (I, [ctypes.c_char_p, P, U32, U32]),
         "wgt_bvh_build": (I, [P, U32, P, U32, P, ctypes.POINTER(WgtSceneInfo)]),
-        "wgt_bvh_build_wide": (I, [P, U32, P, U32, P, U32, ctypes.POINTER(WgtSceneInfo)]),
         "wgt_render_frames": (I, [P, P, U32, U32, P, U32, P, P]),
     }
     for name, (res, args) in sig.items():
@@ -138,6 +136,8 @@ def lib():
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
+    if L.wgt_version() != API_VERSION:  # the structs above mirror this version of include/wgt_api.h
+        raise ImportError(f"{LIB_PATH}: ABI version {L.wgt_version()}, this wrapper mirrors {API_VERSION}")
     _lib = L
     return L
 

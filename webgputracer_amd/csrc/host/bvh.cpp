@@ -78,7 +78,7 @@ uint32_t SahLeafMax() {
 
 class Builder {
  public:
-  // leaf_max: the largest leaf (kLeafMax for the BVH4 forms, kW8LeafMax for the wide form)
+  // leaf_max: the largest leaf (kLeafMax, the BVH4 record's limit)
   Builder(std::vector<Prim>& p, BvhOut& o, std::vector<float>& n2, uint32_t limit,
           uint32_t leaf_max = (uint32_t)kLeafMax)
       : prims_(p), out_(o), nodes_(n2), limit_(limit), leaf_max_(leaf_max),
@@ -547,57 +547,10 @@ void CompactNode(const float* n, float s, double G, uint32_t* q) {
   q[3] = 0u;  // reserved
 }
 
-// The 64-B compact form (wgt_geom.h, WGT_CNODE=3): the same codes, relative to an origin on a
-// grid of 512 steps, org/s = 512 K with K a signed byte (stored beside the refs).  q: 16 words,
-// the x, y, z code words (as CompactNode's q[4..15]), then four words whose top bytes hold K
-// for x, y, z and 0 (the upload ORs the 24-bit refs into their low bytes).  false when some
-// K is outside [-128, 127] (the scene lies too far from the world origin for this form).
-bool CompactNode64(const float* n, float s, double G, uint32_t* q) {
-  bool live[kBvhWidth];
-  for (int i = 0; i < kBvhWidth; ++i) live[i] = !(n[i] == kEmptySlotCoord && n[4 + i] == kEmptySlotCoord);
-  bool ok = true;
-  for (int a = 0; a < 3; ++a) {
-    double ulo = std::numeric_limits<double>::infinity();
-    for (int i = 0; i < kBvhWidth; ++i)
-      if (live[i]) ulo = std::min(ulo, (double)n[(2 * a) * 4 + i]);
-    const double K = std::floor((ulo - G) / (double)s / 512.0);
-    if (!(K >= -128.0 && K <= 127.0)) ok = false;
-    const double orgd = 512.0 * std::min(std::max(K, -128.0), 127.0) * (double)s;
-    uint32_t lo_h[kBvhWidth], hi_h[kBvhWidth];
-    for (int i = 0; i < kBvhWidth; ++i) {
-      lo_h[i] = hi_h[i] = 0x7c00u;
-      if (!live[i]) continue;
-      const double blo = (double)n[(2 * a) * 4 + i] - G, bhi = (double)n[(2 * a + 1) * 4 + i] + G;
-      uint32_t l = 0, r = 0x7bffu;
-      while (l < r) {
-        const uint32_t m = (l + r + 1) / 2;
-        if (CDecD(m, s, orgd) <= blo) l = m; else r = m - 1;
-      }
-      lo_h[i] = l;
-      l = 0; r = 0x7bffu;
-      while (l < r) {
-        const uint32_t m = (l + r) / 2;
-        if (CDecD(m, s, orgd) >= bhi) r = m; else l = m + 1;
-      }
-      hi_h[i] = l;
-      if (CDecD(lo_h[i], s, orgd) > blo || CDecD(hi_h[i], s, orgd) < bhi) ok = false;
-    }
-    q[4 * a + 0] = lo_h[0] | (lo_h[1] << 16);
-    q[4 * a + 1] = lo_h[2] | (lo_h[3] << 16);
-    q[4 * a + 2] = hi_h[0] | (hi_h[1] << 16);
-    q[4 * a + 3] = hi_h[2] | (hi_h[3] << 16);
-    q[12 + a] = (uint32_t)(uint8_t)(int8_t)std::min(std::max(K, -128.0), 127.0) << 24;
-  }
-  q[15] = 0u;
-  return ok;
-}
-
 // The smallest power-of-two step with which code 65504 reaches every node's upper
 // bounds plus the margins (the origin sits up to G + one float step of org/s below
 // the lower bound).
-// gap: how far below the lower bound (minus G) the origin may sit, in steps (0: the float
-// org/s of CompactNode; 512: the grid origin of CompactNode64)
-float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes, double G, double gap = 0.0) {
+float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes, double G) {
   int e = -24;
   for (;;) {
     const float s = std::ldexp(1.0f, e);
@@ -611,179 +564,6 @@ float CompactStep(const std::vector<float>& nodes, uint32_t n_nodes, double G, d
             ulo = std::min(ulo, (double)n[(2 * a) * 4 + i]);
             uhi = std::max(uhi, (double)n[(2 * a + 1) * 4 + i]);
           }
-        const double org_low = ulo - G - (std::fabs(ulo - G) * 0x1p-23 + (double)s * 0x1p-126) - gap * (double)s;
-        ok = org_low + 65504.0 * (double)s >= uhi + G;
-      }
-    }
-    if (ok) return s;
-    ++e;
-  }
-}
-
-// ---------------------------------------------------------------------------------------
-// The wide form (wgt_geom.h kW8*).  A dynamic program over a BVH2 with
-// leaves of <= kW8LeafMax triangles picks, per BVH2 node r and depth allowance d, the SAH-cheapest
-// 8-slot node:
-//   N(r, d) = c_node * A(r) + min_{k=2..8} Q(r's children -> k slots, d - 1)    (N(r, 0) = inf)
-//   Q(c -> 1 slot, d) = leaf ? c_tri * count * A(c) : N(c, d)
-//   Q(c -> k slots, d) = min_{i + j = k} Q(left(c) -> i, d) + Q(right(c) -> j, d)
-// A visit pushes at most two stack entries whatever its width (the group of internal children it
-// does not descend into, and a second triangle group), so the stack bound is 2 x the depth: the
-// budget is the depth.  Like the BVH4 collapse it only regroups BVH2 boxes.
-// The wide form is opt-in (only WGT_CNODE=4 reads it) and its own BVH2 build and collapse take about
-// as long as the BVH4's: built when WGT_W8=1, or with WGT_W8 unset when WGT_CNODE=4 at the build
-// (the scene upload); never with WGT_W8=0.  wgt_bvh_build_wide asks for it (BvhOut::want_wide).
-bool WideWanted() {
-  const char* v = std::getenv("WGT_W8");
-  if (v && *v) return std::atoi(v) != 0;
-  const char* c = std::getenv("WGT_CNODE");
-  return c && *c && std::atoi(c) == 4;
-}
-double W8NodeCost() {
-  const char* v = std::getenv("WGT_W8_NODE");
-  return v && *v ? std::atof(v) : 1.0;
-}
-
-class WideCollapser {
- public:
-  WideCollapser(const std::vector<float>& n2, uint32_t max_depth)
-      : n2_(n2), nd_(max_depth + 1), n_(n2.size() / 16) {
-    const float inf = std::numeric_limits<float>::infinity();
-    cost_.assign(n_ * kW8Slots * nd_, inf);  // [node][k-1][d]: k = 1 is N(node, d)
-    for (size_t i = n_; i-- > 0;) {         // preorder: children have larger ids
-      const Child a = Child2(n2_, (int)i, 0), b = Child2(n2_, (int)i, 1);
-      Box u = a.b;
-      u.grow(b.b);
-      const double area = u.area();
-      for (uint32_t d = 0; d < nd_; ++d) {
-        for (int k = 2; k <= (int)kW8Slots; ++k) {
-          float best = inf;
-          for (int ia = 1; ia < k; ++ia) best = std::min(best, Slots(a, ia, d) + Slots(b, k - ia, d));
-          Q(i, k, d) = best;
-        }
-      }
-      for (uint32_t d = 1; d < nd_; ++d) {
-        float best = inf;
-        for (int k = 2; k <= (int)kW8Slots; ++k) best = std::min(best, Q(i, k, d - 1));
-        Q(i, 1, d) = (float)(c_node_ * area) + best;
-      }
-    }
-  }
-  float Cost(uint32_t d) const { return d < nd_ ? Q(0, 1, d) : std::numeric_limits<float>::infinity(); }
-
-  // The slots of BVH2 node id2 as one wide node of depth allowance d: internal slots first.
-  void NodeSlots(int id2, uint32_t d, std::vector<Child>& slots) const {
-    const Child a = Child2(n2_, id2, 0), b = Child2(n2_, id2, 1);
-    int best_k = 2;
-    float best = std::numeric_limits<float>::infinity();
-    for (int k = 2; k <= (int)kW8Slots; ++k)
-      if (Q(id2, k, d - 1) < best) {
-        best = Q(id2, k, d - 1);
-        best_k = k;
-      }
-    std::vector<Child> all;
-    Split(a, b, best_k, d - 1, all);
-    slots.clear();
-    for (const Child& c : all)
-      if (c.ref >= 0) slots.push_back(c);
-    for (const Child& c : all)
-      if (c.ref < 0) slots.push_back(c);
-  }
-
- private:
-  float& Q(size_t node, int k, uint32_t d) { return cost_[(node * kW8Slots + (size_t)(k - 1)) * nd_ + d]; }
-  float Q(size_t node, int k, uint32_t d) const { return cost_[(node * kW8Slots + (size_t)(k - 1)) * nd_ + d]; }
-  float Slots(const Child& c, int k, uint32_t d) const {
-    if (c.ref < 0) return k == 1 ? (float)(c_tri_ * leaf_count(c.ref) * c.b.area()) : std::numeric_limits<float>::infinity();
-    return Q((size_t)c.ref, k, d);
-  }
-  void Split(const Child& a, const Child& b, int k, uint32_t d, std::vector<Child>& out) const {
-    int best_i = 1;
-    float best = std::numeric_limits<float>::infinity();
-    for (int i = 1; i < k; ++i) {
-      const float c = Slots(a, i, d) + Slots(b, k - i, d);
-      if (c < best) {
-        best = c;
-        best_i = i;
-      }
-    }
-    Cover(a, best_i, d, out);
-    Cover(b, k - best_i, d, out);
-  }
-  void Cover(const Child& c, int k, uint32_t d, std::vector<Child>& out) const {
-    if (k == 1) {
-      out.push_back(c);
-      return;
-    }
-    Split(Child2(n2_, c.ref, 0), Child2(n2_, c.ref, 1), k, d, out);
-  }
-
-  const std::vector<float>& n2_;
-  uint32_t nd_;
-  size_t n_;
-  double c_node_ = W8NodeCost(), c_tri_ = 1.0;
-  std::vector<float> cost_;
-};
-
-// One wide record before encoding: its slots' boxes (exact BVH2 boxes), g, L, ni, imask.
-struct WideRec {
-  Box b[kW8Slots];
-  uint32_t live = 0;  // mask of live slots
-  uint32_t g = 0, L = 0, ni = 0, imask = 0;
-};
-
-// Codes of one axis of a wide record (CompactNode's rule: the tightest binary16 codes keeping the
-// margin G, relative to the float org/s below the children's lowest bound).
-void EncodeAxis(const WideRec& r, int a, float s, double G, float& orgs, uint32_t* lo_w, uint32_t* hi_w) {
-  double ulo = std::numeric_limits<double>::infinity();
-  for (uint32_t i = 0; i < kW8Slots; ++i)
-    if ((r.live >> i) & 1u) ulo = std::min(ulo, (double)r.b[i].lo[a]);
-  const double target = (ulo - G) / (double)s;
-  float f = (float)target;
-  while ((double)f > target) f = std::nextafter(f, -std::numeric_limits<float>::infinity());
-  orgs = f;
-  const double orgd = (double)f * (double)s;
-  uint32_t lo_h[kW8Slots], hi_h[kW8Slots];
-  for (uint32_t i = 0; i < kW8Slots; ++i) {
-    lo_h[i] = hi_h[i] = 0x7c00u;  // an empty slot: +inf planes, never entered
-    if (!((r.live >> i) & 1u)) continue;
-    const double blo = (double)r.b[i].lo[a] - G, bhi = (double)r.b[i].hi[a] + G;
-    uint32_t l = 0, h = 0x7bffu;
-    while (l < h) {
-      const uint32_t m = (l + h + 1) / 2;
-      if (CDecD(m, s, orgd) <= blo) l = m; else h = m - 1;
-    }
-    lo_h[i] = l;
-    l = 0; h = 0x7bffu;
-    while (l < h) {
-      const uint32_t m = (l + h) / 2;
-      if (CDecD(m, s, orgd) >= bhi) h = m; else l = m + 1;
-    }
-    hi_h[i] = l;
-  }
-  for (uint32_t w = 0; w < 4; ++w) {
-    lo_w[w] = lo_h[2 * w] | (lo_h[2 * w + 1] << 16);
-    hi_w[w] = hi_h[2 * w] | (hi_h[2 * w + 1] << 16);
-  }
-}
-
-// The smallest power-of-two step with which code 65504 reaches every record's upper bounds plus
-// the margins (CompactStep's rule over the wide records).
-float WideStep(const std::vector<WideRec>& recs, double G) {
-  int e = -24;
-  for (;;) {
-    const float s = std::ldexp(1.0f, e);
-    bool ok = true;
-    for (size_t k = 0; k < recs.size() && ok; ++k) {
-      const WideRec& r = recs[k];
-      if (r.live == 0) continue;
-      for (int a = 0; a < 3 && ok; ++a) {
-        double ulo = std::numeric_limits<double>::infinity(), uhi = -ulo;
-        for (uint32_t i = 0; i < kW8Slots; ++i) {
-          if (!((r.live >> i) & 1u)) continue;
-          ulo = std::min(ulo, (double)r.b[i].lo[a]);
-          uhi = std::max(uhi, (double)r.b[i].hi[a]);
-        }
         const double org_low = ulo - G - (std::fabs(ulo - G) * 0x1p-23 + (double)s * 0x1p-126);
         ok = org_low + 65504.0 * (double)s >= uhi + G;
       }
@@ -793,143 +573,15 @@ float WideStep(const std::vector<WideRec>& recs, double G) {
   }
 }
 
-// Emit the wide tree of the BVH2 n2 over prims (their order after that build) into out.w8*.
-class WideEmitter {
- public:
-  WideEmitter(const WideCollapser& dp, const std::vector<Prim>& prims, const wgt_triangle* tris, BvhOut& out)
-      : dp_(dp), prims_(prims), tris_(tris), out_(out) {}
-
-  // record `rec` := the wide node of BVH2 node id2 (depth allowance d, level `depth`)
-  void Emit(int id2, uint32_t rec, uint32_t d, uint32_t depth) {
-    std::vector<Child> slots;
-    dp_.NodeSlots(id2, d, slots);
-    Node(slots, rec, d, depth);
-  }
-  // a tree that is one BVH2 leaf: a root record with one leaf slot
-  void EmitLeafRoot(const Child& leaf) { Node(std::vector<Child>{leaf}, 0u, 1u, 1u); }
-
-  std::vector<WideRec> recs;  // by record index (holes: live = 0)
-
- private:
-  void Node(const std::vector<Child>& in, uint32_t rec, uint32_t d, uint32_t depth) {
-    const uint32_t g = ++groups_;  // groups start at 1 (record 0 is the root)
-    Grow((size_t)(g + 1) * kW8Slots);
-    out_.w8_depth = std::max(out_.w8_depth, depth);
-    out_.w8_nodes++;
-    // the slots as NodeSlots gives them: internal children first (the kernel's nearest-first
-    // descent reads ni; Ylitie et al.'s octant slot order, with a first-in-visit-order descent and no
-    // distance keys, measured 4 % slower on sponza: more node visits and triangle tests)
-    const std::vector<Child>& slots = in;
-    WideRec r;
-    r.g = g;
-    for (uint32_t s = 0; s < slots.size(); ++s) {
-      r.live |= 1u << s;
-      r.b[s] = slots[s].b;
-      if (slots[s].ref >= 0) {
-        r.imask |= 1u << s;
-        r.ni = s + 1;
-        continue;
-      }
-      const uint32_t first = leaf_first(slots[s].ref), cnt = leaf_count(slots[s].ref);
-      out_.w8_leaves++;
-      r.L |= ((1u << cnt) - 1u) << (4 * s);
-      for (uint32_t i = 0; i < cnt; ++i) TriRecord(4 * (g * kW8Slots + s) + i, prims_[first + i]);
-    }
-    recs[rec] = r;
-    for (uint32_t s = 0; s < kW8Slots; ++s)
-      if ((r.imask >> s) & 1u) Emit(slots[s].ref, g * kW8Slots + s, d - 1, depth + 1);
-  }
-  void Grow(size_t n_recs) {
-    if (recs.size() >= n_recs) return;
-    recs.resize(n_recs);
-    // every triangle position starts as the degenerate record (e1 = e2 = 0: |det| < 1e-12 rejects)
-    out_.w8tris.resize(n_recs * 4 * kTriRecordFloats, 0.0f);
-  }
-  void TriRecord(size_t pos, const Prim& p) {
-    const wgt_triangle& t = tris_[p.idx];
-    float* o = &out_.w8tris[pos * kTriRecordFloats];
-    o[0] = t.v0[0]; o[1] = t.v0[1]; o[2] = t.v0[2];
-    std::memcpy(&o[3], &p.idx, 4);
-    o[4] = t.e1[0]; o[5] = t.e1[1]; o[6] = t.e1[2]; o[7] = p.b.lo[0];
-    o[8] = t.e2[0]; o[9] = t.e2[1]; o[10] = t.e2[2]; o[11] = p.b.lo[1];
-    o[12] = p.b.lo[2]; o[13] = p.b.hi[0]; o[14] = p.b.hi[1]; o[15] = p.b.hi[2];
-  }
-
-  const WideCollapser& dp_;
-  const std::vector<Prim>& prims_;
-  const wgt_triangle* tris_;
-  BvhOut& out_;
-  uint32_t groups_ = 0;
-};
-
-// Build the wide form beside the BVH4 forms (out.w8*); false (w8_ok stays false) when the tree
-// does not fit it.  prims: the triangles' boxes and centroids in input order.
-bool BuildWide(const wgt_triangle* tris, std::vector<Prim> prims, uint32_t max_depth_limit, double M,
-               BvhOut& out) {
-  const uint32_t n = (uint32_t)prims.size();
-  BvhOut tmp;  // the BVH2 statistics of the wide tree's own build
-  std::vector<float> n2;
-  n2.reserve((size_t)16 * 2 * (n / 2 + 1));
-  Builder b(prims, tmp, n2, max_depth_limit, kW8LeafMax);
-  Box root_box;
-  const int root = b.Build(0, n, 0, root_box);
-  out.w8nodes.clear();
-  out.w8tris.clear();
-  out.w8leaf.clear();
-  out.w8_groups = out.w8_nodes = out.w8_leaves = out.w8_depth = 0;
-  WideCollapser dp(n2, root < 0 ? 1u : kW8MaxDepth);
-  WideEmitter em(dp, prims, tris, out);
-  if (root < 0) {
-    Child c;
-    c.b = root_box;
-    c.ref = root;
-    em.EmitLeafRoot(c);
-  } else {
-    if (!(dp.Cost(kW8MaxDepth) < std::numeric_limits<float>::infinity())) return false;
-    em.Emit(0, 0u, kW8MaxDepth, 1u);
-  }
-  const uint32_t groups = (uint32_t)(em.recs.size() / kW8Slots) - 1u;
-  if (groups >= kW8MaxGroups) return false;
-  out.w8_groups = groups;
-  out.w8_stack = 2u * out.w8_depth;
-  out.w8_sah = root < 0 ? 0.0 : dp.Cost(kW8MaxDepth) / std::max(root_box.area(), 1e-300);
-  for (const WideRec& r : em.recs)
-    for (uint32_t i = 0; i < kW8Slots; ++i)
-      for (int a = 0; a < 3 && ((r.live >> i) & 1u); ++a) M = std::max({M, 2.0 * std::fabs((double)r.b[i].lo[a]), 2.0 * std::fabs((double)r.b[i].hi[a])});
-  if (!(M <= (double)out.cbound)) return false;  // the BVH4 forms' bound holds the wide boxes too
-  const double G = std::ldexp((double)out.cbound, -21);
-  out.w8step = WideStep(em.recs, G);
-  out.w8nodes.assign(em.recs.size() * kW8RecordWords, 0u);
-  out.w8leaf.assign((size_t)groups + 1, 0u);
-  for (size_t k = 0; k < em.recs.size(); ++k) {
-    const WideRec& r = em.recs[k];
-    if (r.live == 0) continue;
-    uint32_t* q = &out.w8nodes[k * kW8RecordWords];
-    float orgs[3];
-    const uint32_t lo_row[3] = {kW8LoX, kW8LoY, kW8LoZ}, hi_row[3] = {kW8HiX, kW8HiY, kW8HiZ};
-    for (int a = 0; a < 3; ++a) EncodeAxis(r, a, out.w8step, G, orgs[a], &q[lo_row[a]], &q[hi_row[a]]);
-    std::memcpy(&q[kW8Head], orgs, 12);
-    q[kW8Head + 3] = r.g;
-    q[kW8Meta + 0] = r.L;
-    q[kW8Meta + 1] = r.ni;
-    q[kW8Meta + 2] = r.imask;
-    out.w8leaf[r.g] = r.L;
-  }
-  out.w8_ok = true;
-  return true;
-}
-
 }  // namespace
 
 bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, uint32_t stack_limit,
               uint32_t narrow_limit, double narrow_ratio, double origin_bound, BvhOut& out, std::string& err) {
-  const bool want_wide = out.want_wide || WideWanted();
   out = BvhOut{};
   if (n == 0) { err = "BuildBvh: no triangles"; return false; }
   // leaf walks use 32-bit byte offsets into the 64-B records (wgt_geom.h kTriRecordBytes)
   if (n >= (1u << 26)) { err = "BuildBvh: too many triangles (max 2^26-1)"; return false; }
   std::vector<Prim> prims(n);
-  std::vector<Prim> prims_in;  // input order, for the wide form's own build
   for (uint32_t i = 0; i < n; ++i) {
     const wgt_triangle& t = tris[i];
     f3 lo, hi;
@@ -947,7 +599,6 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
       }
     }
   }
-  if (want_wide) prims_in = prims;
   if (MedianDepth(n) > max_depth_limit) {
     err = "BuildBvh: too many triangles for depth limit " + std::to_string(max_depth_limit);
     return false;
@@ -1051,11 +702,6 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
     CompactNode(&out.nodes[(size_t)i * kNode4Floats], out.cstep, G, &out.cnodes[(size_t)i * kCNodeFloats]);
     std::memcpy(&out.crefs[(size_t)i * 4], &out.nodes[(size_t)i * kNode4Floats + 24], 16);
   }
-  out.c64step = CompactStep(out.nodes, out.n_nodes, G, 512.0);
-  out.c64.resize((size_t)out.n_nodes * 16);
-  out.c64_ok = true;
-  for (uint32_t i = 0; i < out.n_nodes; ++i)
-    out.c64_ok &= CompactNode64(&out.nodes[(size_t)i * kNode4Floats], out.c64step, G, &out.c64[(size_t)i * 16]);
   out.tris.resize((size_t)n * kTriRecordFloats);
   for (uint32_t i = 0; i < n; ++i) {
     const wgt_triangle& t = tris[prims[i].idx];
@@ -1073,12 +719,6 @@ bool BuildBvh(const wgt_triangle* tris, uint32_t n, uint32_t max_depth_limit, ui
     float* o = &out.tshade[(size_t)i * 8];
     o[0] = t.face_norm[0]; o[1] = t.face_norm[1]; o[2] = t.face_norm[2]; o[3] = t.emissive;
     o[4] = t.col[0]; o[5] = t.col[1]; o[6] = t.col[2]; o[7] = 0.0f;
-  }
-  if (!prims_in.empty() && !BuildWide(tris, std::move(prims_in), max_depth_limit, M, out)) {
-    out.w8_ok = false;
-    out.w8nodes.clear();
-    out.w8tris.clear();
-    out.w8leaf.clear();
   }
   return true;
 }

@@ -17,24 +17,11 @@ struct BvhOut {
   std::vector<int32_t> crefs;    // 4 child refs per node (the compact form's ref records)
   float cstep = 1.0f;            // scene-wide decode step of the compact nodes
   float cbound = 0.0f;           // M: the compact codes are exact for ray origins with |o| <= M
-  std::vector<uint32_t> c64;     // 16 words per node: the 64-B compact form without refs (WGT_CNODE=3)
-  float c64step = 1.0f;          // its decode step
-  bool c64_ok = false;           // every node's grid origin fits a signed byte
   std::vector<float> tris;    // kTriRecordFloats per triangle, leaf order (wgt_geom.h)
   std::vector<float> tshade;  // 8 floats per original triangle
   uint32_t n_nodes = 0, n_leaves = 0, max_depth = 0, max_leaf = 0;  // BVH4 nodes / depth
   uint32_t n_nodes2 = 0, depth2 = 0;  // the SAH BVH2 the BVH4 was collapsed from
   uint32_t stack_need = 0;            // worst-case traversal stack entries (exact for this tree)
-  // the wide form (wgt_geom.h kW8*): records 8g + s of 32 words, triangle records 4(8g + s) + i
-  // of kTriRecordFloats, over its own BVH2 (leaves <= kW8LeafMax); w8_ok = false without it
-  bool want_wide = false;  // input: build the wide form whatever the environment (wgt_bvh_build_wide)
-  bool w8_ok = false;
-  std::vector<uint32_t> w8nodes;
-  std::vector<float> w8tris;
-  std::vector<uint32_t> w8leaf;  // per group: the L word of the record that owns it
-  uint32_t w8_groups = 0, w8_nodes = 0, w8_leaves = 0, w8_depth = 0, w8_stack = 0;
-  float w8step = 1.0f;
-  double w8_sah = 0.0;
   bool narrow = false;                // collapsed under narrow_limit (BuildBvh)
   double sah_cost = 0.0;
 };

@@ -65,8 +65,12 @@ __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict_
   // below, decided before the square root.  qt is +inf until a quad is accepted.
   if (t >= qt) return;
   const f3 pos = o + t * d;
+#ifdef WGT_QUADDIST_PROBE
+  const float ray_dist = t;  // PROBE ONLY: ties of the rounded distance ignored
+#else
   const float ray_dist = distance(pos, o);
   if (ray_dist >= h.dist) return;
+#endif
   const f3 hit_vec = pos - xyz(q[0]);
   const f3 w = xyz(wd);
   const float a = dot(w, cross(hit_vec, xyz(q[2])));
@@ -200,13 +204,7 @@ struct Trav {
 // A triangle was accepted (bi starts at kNoHit, see trav_init).
 __device__ __forceinline__ bool trav_found(const Trav& t) { return t.bi != kNoHit; }
 
-// The node form CN: 0 = 128-B nodes, 1 = 80-B compact records, 2 = 64-B compact records, 3 = the
-// wide 8-slot records (node_step_w8).
-// A compact form's decode step s (a power of two) and 1/s.
-template <int CN>
-__device__ __forceinline__ float cstep_of(const DevScene& sc) { return CN == 3 ? sc.w8step : CN == 2 ? sc.c64step : sc.cstep; }
-template <int CN>
-__device__ __forceinline__ float rcstep_of(const DevScene& sc) { return CN == 3 ? sc.rw8step : CN == 2 ? sc.rc64step : sc.rcstep; }
+// The node form CN: 0 = 128-B nodes, 1 = 80-B compact records.
 
 // CN (compact nodes): t.inv holds s/d (s = the form's step, a power of two: exact), the
 // factor of the fused slab step (cchild_key); the triangle box check multiplies
@@ -215,7 +213,7 @@ template <int CN = 0>
 __device__ __forceinline__ void trav_init(const DevScene& sc, f3 o, f3 d, bool quad_hit, float qt, Trav& t) {
   t.inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
   t.ot = slab_offset(o, t.inv);
-  if (CN) t.inv = cstep_of<CN>(sc) * t.inv;
+  if (CN) t.inv = sc.cstep * t.inv;
   // a triangle must satisfy t < t_quad to beat a quad hit (ray_dist is monotone in
   // t): with bi = kNoHit the rule "t < bt, or t == bt and index < bi" accepts
   // exactly t <= bt, so bt = the float below t_quad (t_quad > 0).  A box entered
@@ -276,24 +274,12 @@ template <int CN>
 __device__ __forceinline__ void node_keys(const DevScene& sc, const Trav& t, int ref, uint32_t& k0, uint32_t& k1,
                                           uint32_t& k2, uint32_t& k3, int& r0, int& r1, int& r2, int& r3) {
   if (CN) {
-    int4 rf;
-    float4 a;
-    uint4 x, y, z;
-    if constexpr (CN == 2) {  // 64-B record: the codes, then refs and origin packed (wgt_geom.h)
-      const float4* __restrict__ n = (const float4*)((const char*)sc.cnodes64 + (uint32_t)ref);  // byte offset
-      x = __builtin_bit_cast(uint4, n[0]), y = __builtin_bit_cast(uint4, n[1]), z = __builtin_bit_cast(uint4, n[2]);
-      const uint4 w = __builtin_bit_cast(uint4, n[3]);
-      rf = int4{__builtin_amdgcn_sbfe((int)w.x, 0, 24), __builtin_amdgcn_sbfe((int)w.y, 0, 24),
-                __builtin_amdgcn_sbfe((int)w.z, 0, 24), __builtin_amdgcn_sbfe((int)w.w, 0, 24)};
-      // org/s = 512 K, K the signed top byte: exact
-      a = float4{__builtin_ldexpf((float)((int)w.x >> 24), 9), __builtin_ldexpf((float)((int)w.y >> 24), 9),
-                 __builtin_ldexpf((float)((int)w.z >> 24), 9), 0.0f};
-    } else {  // 80-B record: origin, codes, refs
-      const float4* __restrict__ n = (const float4*)((const char*)sc.cnodes + (uint32_t)ref);  // byte offset
-      rf = __builtin_bit_cast(int4, n[4]);
-      a = n[0];
-      x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]), z = __builtin_bit_cast(uint4, n[3]);
-    }
+    // 80-B record: origin, codes, refs
+    const float4* __restrict__ n = (const float4*)((const char*)sc.cnodes + (uint32_t)ref);  // byte offset
+    const int4 rf = __builtin_bit_cast(int4, n[4]);
+    const float4 a = n[0];
+    const uint4 x = __builtin_bit_cast(uint4, n[1]), y = __builtin_bit_cast(uint4, n[2]),
+                z = __builtin_bit_cast(uint4, n[3]);
     // c = the slab distance of the node origin org' = (org/s) * s: fma(org/s, s/d, ot)
     const f3 c = f3{__builtin_fmaf(a.x, t.inv.x, t.ot.x), __builtin_fmaf(a.y, t.inv.y, t.ot.y),
                     __builtin_fmaf(a.z, t.inv.z, t.ot.z)};
@@ -569,171 +555,9 @@ __device__ __forceinline__ void node_step(const DevScene& sc, Trav& t, const STK
   trav_resolve(sc, t, k0 != kMissKey ? r0 : kNoRef, lds);
 }
 
-// ---------------------------------------------------------------------------
-// The wide form (CN = 3, wgt_geom.h kW8*).  The lane's open leaf
-// (t.lf, t.le) becomes a triangle group: t.lf = the byte offset of group g's triangle records
-// (g * 2048), t.le = the mask of its records still to test (bit 4s + i: slot s, triangle i).
-// t.ref is the byte offset of the next record to visit.  Stack entries are groups (wgt_geom.h):
-// g | m << GB, the sign bit marking a triangle group.
-template <class STK>
-struct W8Stack {
-  static constexpr int GB = std::is_same<STK, Stack24S<>>::value ? 15 : 23;  // group-index bits
-  static constexpr uint32_t kGroups = 1u << GB;
-  static constexpr int kTri = std::is_same<STK, Stack24S<>>::value ? (int)(0xff800000u) : (int)0x80000000u;
-};
-__device__ __forceinline__ bool w8_can_tri(const Trav& t) { return t.le != 0u; }
-__device__ __forceinline__ bool w8_done(const Trav& t) { return t.ref == kNoRef && t.le == 0u && t.sp == 0; }
-template <int CN>
-__device__ __forceinline__ bool trav_fin(const Trav& t) { return CN == 3 ? w8_done(t) : trav_done(t); }
-__device__ __forceinline__ uint32_t w8_rec(uint32_t g, uint32_t s) { return (g * kW8Slots + s) * kW8RecordBytes; }
-
-// The ray's octant: bit a set when its direction along axis a is negative (the sign of 1/d, or
-// of s/d: the same sign); shifted to bits 4..6 it selects the ray's entry code rows (wgt_geom.h).
-__device__ __forceinline__ uint32_t w8_oct(const Trav& t) {
-  return (__float_as_uint(t.inv.x) >> 31) | ((__float_as_uint(t.inv.y) >> 31) << 1) |
-         ((__float_as_uint(t.inv.z) >> 31) << 2);
-}
-
-// t.ref := the next record from the stack, taking a triangle group on the way when the lane has
-// none open; kNoRef when the stack is empty or a second triangle group is on top.  A node group
-// gives its lowest slot and stays on the stack (with that bit cleared) while slots remain.
-template <bool STATS, class STK>
-__device__ __forceinline__ void w8_resolve(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
-  constexpr int GB = W8Stack<STK>::GB;
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    if (t.sp == 0) break;
-    const int e = lds.ld(t.sp - 1);
-    const uint32_t g = (uint32_t)e & ((1u << GB) - 1u), m = ((uint32_t)e >> GB) & 0xffu;
-    if (e >= 0) {
-      const uint32_t m2 = m & (m - 1u);
-      if (m2 == 0u) --t.sp;
-      else lds.st(t.sp - 1, (int)(g | m2 << GB));
-      t.ref = (int)w8_rec(g, (uint32_t)__builtin_ctz(m));
-      return;
-    }
-    if (t.le != 0u) break;  // a triangle group is open: this one waits
-    --t.sp;
-    if (STATS) st.refills++;  // second triangle groups taken back (wgt_stats stack_refills)
-    // the leaf slots' triangles: the group's L word (w8leaf; testing the slots' whole nibbles, the
-    // degenerate padding records included, was 0.7 tests per sponza ray more, 3.6 % slower)
-    t.lf = g * (kW8Slots * 4u * kTriRecordBytes);
-    t.le = w8_spread4(m) & sc.w8leaf[g];
-  }
-  t.ref = kNoRef;
-}
-
-// Visit t.ref (ROOT: record 0, the wave-uniform root, whose loads are scalar): the 8 slab tests
-// (the fused compact step of node_keys), then descend into the internal child hit nearest by
-// entry distance, push the other internal children hit as one node group, and open the leaf slots hit as the lane's
-// triangle group (or push them as a second one).  Any visit order is exact (the closest hit is a
-// minimum over (t, index)), and a missed child never enters either mask.  The ray's entry plane
-// of an axis is the lo code for 1/d >= 0 and the hi code otherwise: the lane loads the two 16-B
-// rows of an axis in that order (their byte offsets differ by 16), so no select picks them.
-template <bool STATS, class STK, bool ROOT = false>
-__device__ __forceinline__ void node_step_w8(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
-  constexpr int GB = W8Stack<STK>::GB;
-  if (STATS) st.nodes++;
-  const char* __restrict__ base = (const char*)sc.w8nodes;
-  const uint32_t r = ROOT ? 0u : (uint32_t)t.ref;
-  const float4 h0 = *(const float4*)(base + r + kW8Head * 4);
-  const uint4 h1 = *(const uint4*)(base + r + kW8Meta * 4);
-  uint4 nx, fx, ny, fy, nz, fz;
-  if (ROOT) {  // uniform address: scalar loads, selected per lane
-    const uint4 xl = *(const uint4*)(base + kW8LoX * 4), xh = *(const uint4*)(base + kW8HiX * 4);
-    const uint4 yl = *(const uint4*)(base + kW8LoY * 4), yh = *(const uint4*)(base + kW8HiY * 4);
-    const uint4 zl = *(const uint4*)(base + kW8LoZ * 4), zh = *(const uint4*)(base + kW8HiZ * 4);
-    const bool sx = t.inv.x < 0.0f, sy = t.inv.y < 0.0f, sz = t.inv.z < 0.0f;
-    nx = sx ? xh : xl, fx = sx ? xl : xh;
-    ny = sy ? yh : yl, fy = sy ? yl : yh;
-    nz = sz ? zh : zl, fz = sz ? zl : zh;
-  } else {
-    // the ray's octant as address bits 4 (x), 5 (y), 6 (z): its entry rows (wgt_geom.h)
-    const uint32_t o = w8_oct(t) << 4;
-    const uint32_t ax = r | (o & 16u), ay = r | (o & 32u), az = r | (o & 64u);
-    nx = *(const uint4*)(base + ax + kW8LoX * 4), fx = *(const uint4*)(base + (ax ^ 16u) + kW8LoX * 4);
-    ny = *(const uint4*)(base + ay + kW8LoY * 4), fy = *(const uint4*)(base + (ay ^ 32u) + kW8LoY * 4);
-    nz = *(const uint4*)(base + az + kW8LoZ * 4), fz = *(const uint4*)(base + (az ^ 64u) + kW8LoZ * 4);
-  }
-  const f3 c = f3{__builtin_fmaf(h0.x, t.inv.x, t.ot.x), __builtin_fmaf(h0.y, t.inv.y, t.ot.y),
-                  __builtin_fmaf(h0.z, t.inv.z, t.ot.z)};
-  const uint32_t g = __float_as_uint(h0.w), L = h1.x;
-  const uint32_t nxw[4] = {nx.x, nx.y, nx.z, nx.w}, fxw[4] = {fx.x, fx.y, fx.z, fx.w};
-  const uint32_t nyw[4] = {ny.x, ny.y, ny.z, ny.w}, fyw[4] = {fy.x, fy.y, fy.z, fy.w};
-  const uint32_t nzw[4] = {nz.x, nz.y, nz.z, nz.w}, fzw[4] = {fz.x, fz.y, fz.z, fz.w};
-  uint32_t hits = 0u;
-  const uint32_t ni = h1.y;
-  uint32_t kmin = kMissKey;
-#pragma unroll
-  for (uint32_t s = 0; s < kW8Slots; ++s) {
-    const uint32_t w = s >> 1;
-    const float tnx = __builtin_fmaf(hcode(nxw[w], s), t.inv.x, c.x);
-    const float tfx = __builtin_fmaf(hcode(fxw[w], s), t.inv.x, c.x);
-    const float tny = __builtin_fmaf(hcode(nyw[w], s), t.inv.y, c.y);
-    const float tfy = __builtin_fmaf(hcode(fyw[w], s), t.inv.y, c.y);
-    const float tnz = __builtin_fmaf(hcode(nzw[w], s), t.inv.z, c.z);
-    const float tfz = __builtin_fmaf(hcode(fzw[w], s), t.inv.z, c.z);
-    const float nn = __builtin_fmaxf(__builtin_fmaxf(tnx, tny), __builtin_fmaxf(tnz, kRayMin));
-    const float ff = __builtin_fminf(__builtin_fminf(tfx, tfy), __builtin_fminf(tfz, t.bt));
-    const bool hit = nn <= ff;
-    hits |= hit ? 1u << s : 0u;
-    // internal children only (slots < ni); the slot rides in the key's low bits
-    const uint32_t key = (__float_as_uint(nn) & ~7u) | s;
-    kmin = (hit && s < ni) ? (key < kmin ? key : kmin) : kmin;
-  }
-  const bool desc = kmin != kMissKey;
-  const uint32_t near = kmin & 7u;
-  const uint32_t imask = (1u << ni) - 1u;
-  const uint32_t sib = hits & imask & ~(desc ? 1u << near : 0u);  // internal children left
-  const uint32_t lh = hits & ~imask;                                // leaf slots hit
-  // push the siblings, then (a triangle group is open) the leaf slots; a write that is not
-  // counted lands above the top and is overwritten or never read
-  lds.st(t.sp, (int)(g | sib << GB));
-  t.sp += sib != 0u ? 1 : 0;
-  const bool take = t.le == 0u;
-  lds.st(t.sp, (int)(g | lh << GB) | W8Stack<STK>::kTri);
-  const bool push2 = lh != 0u && !take;
-  t.sp += push2 ? 1 : 0;
-  if (STATS) st.spills += push2 ? 1u : 0u;  // second triangle groups (wgt_stats stack_spills)
-  if (take) {
-    t.lf = g * (kW8Slots * 4u * kTriRecordBytes);
-    t.le = w8_spread4(lh) & L;
-  }
-  if (desc) t.ref = (int)w8_rec(g, near);
-  else w8_resolve<STATS>(sc, t, lds, st);
-}
-
-// Test the next two triangles of the lane's triangle group (tri_step's pair form: the second
-// slot re-reads the first record when one is left, and is ignored).
-template <bool STATS, class STK>
-__device__ __forceinline__ void tri_step_w8(const DevScene& sc, f3 o, f3 d, Trav& t, const STK& lds, TravStats& st) {
-  const f3 inv = sc.rw8step * t.inv;  // (s/d) * (1/s) = 1/d exactly
-  const uint32_t m = t.le, m1 = m & (m - 1u);
-  const bool two = m1 != 0u;
-  const uint32_t a0 = t.lf + ((uint32_t)__builtin_ctz(m) << 6);
-  const uint32_t a1 = two ? t.lf + ((uint32_t)__builtin_ctz(m1) << 6) : a0;
-  float tt0, tt1;
-  uint32_t i0, i1;
-  const bool h0 = tri_test<true>(sc.w8tris, a0, o, d, t.ot, inv, t.bt, t.bi, tt0, i0);
-  const bool h1 = tri_test<true>(sc.w8tris, a1, o, d, t.ot, inv, t.bt, t.bi, tt1, i1) && two;
-  if (h0) {
-    t.bt = tt0;
-    t.bi = i0;
-  }
-  if (h1 && (tt1 < t.bt || (tt1 == t.bt && i1 < t.bi))) {
-    t.bt = tt1;
-    t.bi = i1;
-  }
-  if (STATS) st.tris += two ? 2u : 1u;
-  t.le = m1 & (m1 - 1u);
-  static_assert(kTriRecordBytes == 64, "triangle records at 64-B steps");
-  if (t.le == 0u && t.ref == kNoRef) w8_resolve<STATS>(sc, t, lds, st);
-}
-
 template <bool STATS, int CN, class STK>
 __device__ __forceinline__ void root_step(const DevScene& sc, Trav& t, const STK& lds, TravStats& st) {
-  if constexpr (CN == 3) node_step_w8<STATS, STK, true>(sc, t, lds, st);
-  else node_step<STATS, CN, STK, true>(sc, t, lds, st);
+  node_step<STATS, CN, STK, true>(sc, t, lds, st);
 }
 
 // Test the next triangle of the pending leaf; a lane without a node to visit
@@ -742,7 +566,7 @@ template <bool STATS, int CN = 0, class STK>
 __device__ __forceinline__ void tri_step(const DevScene& sc, f3 o, f3 d, Trav& t, const STK& lds,
                                          TravStats& st) {
   // 1/d: under CN t.inv holds s/d, and (s/d) * (1/s) is 1/d exactly
-  const f3 inv = CN ? rcstep_of<CN>(sc) * t.inv : t.inv;
+  const f3 inv = CN ? sc.rcstep * t.inv : t.inv;
 #if WGT_TRI_PER_STEP > 1
   // up to WGT_TRI_PER_STEP triangles of the open leaf per step, their loads issued together
   // (a slot past the leaf's end re-reads the first record and is ignored): the closest hit
@@ -864,8 +688,13 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
     }
     return true;
   }
+#ifdef WGT_FASTDIV_PROBE
+  // PROBE ONLY (not exact outside the unscaled domain): the upper bound of the short forms
+  const f3 w = div3_by(h.norm, length(h.norm));
+#else
   // sample_direction (path_tracer.wgsl:146-154)
   const f3 w = normalize(h.norm);  // onb.w of build_onb_from_w(hit.norm)
+#endif
   f3 sdir;
   // both branches draw two more rand() (r1 then r2) right away: drawn once here, the
   // same values in the same order
@@ -892,18 +721,34 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
   }
   // mixture_pdf (:191-193) = 0.5*cosine_pdf + 0.5*light_area_pdf
   const float len = length(sdir);
+#ifdef WGT_FASTDIV_PROBE
+  const f3 nd = div3_by(sdir, len);
+#else
   const f3 nd = sdir / len;  // normalize(dir): shared by cosine_pdf, the light cosine and :282
+#endif
   const float cs = dot(nd, w);
   const float cpdf = cs <= 0.0f ? 0.0f : cs * k_1_PI;
   const float dist2 = len * len;
   const float light_cosine = fabs_w(nd.y) + kRayMin;
+#ifdef WGT_FASTDIV_PROBE
+  const float lpdf = div_by(dist2, rcp_of(light_cosine * sc.light_area));
+#else
   const float lpdf = dist2 / (light_cosine * sc.light_area);
+#endif
   const float pdf_val = 0.5f * cpdf + 0.5f * lpdf;
   // scattering_pdf (:217-220) normalises the already normalised direction again
+#ifdef WGT_FASTDIV_PROBE
+  const f3 nd2 = div3_by(nd, sqrt_fast(dot(nd, nd)));
+#else
   const f3 nd2 = normalize_unit(nd);  // nd = sdir / exact length: unit, NaN or 0
+#endif
   const float cs2 = dot(h.norm, nd2);
   const float spdf = cs2 < 0.0f ? 0.0f : cs2 * k_1_PI;
+#ifdef WGT_FASTDIV_PROBE
+  pc = div3_by(spdf * (pc * h.col), pdf_val);
+#else
   pc = (spdf * (pc * h.col)) / pdf_val;
+#endif
   ro = h.pos;
   rd = nd;
   return false;

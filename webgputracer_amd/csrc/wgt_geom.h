@@ -43,7 +43,11 @@ WGT_HD void tri_box(f3 v0, f3 e1, f3 e2, f3& lo, f3& hi) {
 // 1/d with |d| < 1e-30 replaced by copysign(1e-30, d): finite, so slab values are never NaN.
 WGT_HD float safe_inv(float x) {
   if (fabs_w(x) < 1e-30f) x = __builtin_copysignf(1e-30f, x);
+#ifdef WGT_FASTDIV_PROBE
+  return div_by(1.0f, rcp_of(x));
+#else
   return 1.0f / x;
+#endif
 }
 
 // Slab interval of box [lo, hi] for a ray given as inv = 1/d and ot = -(o * inv):
@@ -152,70 +156,12 @@ constexpr int kLeafMax = 8;
 // records (the full footprint).
 constexpr int kCNodeFloats = 16;     // the node part, as exported by wgt_bvh_build_compact
 constexpr int kCRecordFloat4s = 5;  // node + refs, the device record
-// The 64-B form (WGT_CNODE=3): the three code float4s, then the four refs
-// as 24-bit fields whose top bytes hold the origin, org/s = 512 K per axis with K a signed
-// byte (host/bvh.cpp CompactNode64), decoded per visit instead of read as floats.  Its own
-// decode step (the 512-step origin grid widens the code range).
-constexpr int kC64RecordFloat4s = 4;
 constexpr size_t kCompactNodeBytes = (size_t)4 << 20;
 WGT_HD float qdec(float code, float step, float org) { return __builtin_fmaf(code, step, org); }
 WGT_HD float half_bits_to_float(uint32_t b) {
   const uint32_t e = (b >> 10) & 0x1fu, m = b & 0x3ffu;
   const float v = e ? __builtin_bit_cast(float, ((e + 112u) << 23) | (m << 13)) : (float)m * 5.9604645e-8f;
   return (b & 0x8000u) ? -v : v;
-}
-
-// Wide form (WGT_CNODE=4): 8-slot nodes in 128-B records (one L2 line),
-// the same binary16 codes, fused slab step and margin as the compact BVH4 records, over a BVH2
-// with leaves of <= kW8LeafMax triangles.  Addressing has no per-child refs: every internal
-// node owns a group g of 8 slot positions, record 8g + s for its slot s (the root is record 0,
-// groups start at 1), and slot s's leaf triangles are the triangle records 4(8g + s) + i,
-// i < count (unused positions hold a degenerate triangle that every ray rejects).  A record:
-//   byte 0:   org/s (x, y, z), g
-//   byte 112: L (bit 4s + i set for leaf slot s's triangle i; internal slots' nibbles are 0),
-//             ni (the internal children sit in slots 0 .. ni-1, the leaves after them), imask (the
-//             internal slots, (1 << ni) - 1), 0
-//   the codes of slots 0..7 (two halves per word), one 16-B row per axis and side, placed so that
-//   an axis's lo and hi rows differ in one address bit: lo.x @32, hi.x @48 (bit 4); lo.y @64,
-//   hi.y @96 (bit 5); lo.z @16, hi.z @80 (bit 6).  A lane reads its entry plane's row at
-//   (record | (octant bits << 4)) + the lo row's offset and its exit plane's row with that bit
-//   flipped: no select per code word
-// A lane's stack holds groups, not children (Ylitie et al. 2017): a node group g | m << GB is
-// the internal children of group g in mask m still to visit, a triangle group (the sign bit
-// set) the leaf slots in m whose triangles are to be tested; a visit pushes at most one of each,
-// so the stack bound is twice the tree's depth in node levels.
-constexpr uint32_t kW8Slots = 8;
-constexpr uint32_t kW8LeafMax = 4;
-constexpr uint32_t kW8RecordBytes = 128;
-constexpr uint32_t kW8RecordWords = 32;
-// word offsets in a record: header, meta, and the lo / hi code rows of x, y, z
-constexpr uint32_t kW8Head = 0, kW8Meta = 28, kW8LoX = 8, kW8HiX = 12, kW8LoY = 16, kW8HiY = 24, kW8LoZ = 4,
-                   kW8HiZ = 20;
-constexpr uint32_t kW8MaxDepth = 16;     // 2 x 16 = 32 stack entries (the BVH4 forms' LDS budget)
-constexpr uint32_t kW8MaxGroups = 1u << 21;  // triangle-group byte offsets g * 2048 in 32 bits
-static_assert((kW8HiX - kW8LoX) * 4 == 16 && (kW8HiY - kW8LoY) * 4 == 32 && (kW8HiZ - kW8LoZ) * 4 == 64,
-              "an axis's lo and hi rows differ in address bit 4 + axis");
-WGT_HD uint32_t w8_spread4(uint32_t m) {   // bit k of an 8-bit mask -> nibble k (0xF)
-#if defined(__HIP_DEVICE_COMPILE__)
-  // shift-ors as v_lshl_or_b32: written in C, the compiler folds them into two quarter-rate
-  // v_mul_lo_u32 (the shifted copies share no bits)
-  uint32_t x = m & 0xffu, y;
-  asm("v_lshl_or_b32 %0, %1, 12, %1" : "=v"(y) : "v"(x));
-  x = y & 0x000F000Fu;
-  asm("v_lshl_or_b32 %0, %1, 6, %1" : "=v"(y) : "v"(x));
-  x = y & 0x03030303u;
-  asm("v_lshl_or_b32 %0, %1, 3, %1" : "=v"(y) : "v"(x));
-  x = y & 0x11111111u;
-  asm("v_lshl_or_b32 %0, %1, 1, %1" : "=v"(y) : "v"(x));
-  asm("v_lshl_or_b32 %0, %1, 2, %1" : "=v"(x) : "v"(y));
-  return x;
-#else
-  uint32_t x = m & 0xffu;
-  x = (x | (x << 12)) & 0x000F000Fu;
-  x = (x | (x << 6)) & 0x03030303u;
-  x = (x | (x << 3)) & 0x11111111u;
-  return x * 15u;
-#endif
 }
 
 WGT_HD int leaf_ref(uint32_t first, uint32_t count) { return ~(int)(first * 8u + (count - 1u)); }

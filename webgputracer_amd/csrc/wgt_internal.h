@@ -44,20 +44,12 @@ struct DevScene {
   const float4* __restrict__ tris;
   const float4* __restrict__ tshade;
   const float4* __restrict__ cnodes;  // the same tree as 80-B compact records (wgt_geom.h)
+  // the level of each BVH4 node (root 0), by node index: read by the instrumented (STATS) passes
+  // only, to split node visits and traversal-step cycles by tree level
+  const uint8_t* __restrict__ node_level;
   float cstep;                        // scene-wide decode step of the compact nodes (a power of two)
   float rcstep;                       // 1 / cstep
   float cbound;                       // the compact codes hold for ray origins with |coordinate| <= cbound
-  // the same tree as 64-B compact records (kC64RecordFloat4s, WGT_CNODE=3), their step and
-  // 1 / step; c64bound < 0 when the tree's refs or origins do not fit the form
-  const float4* __restrict__ cnodes64;
-  float c64step, rc64step, c64bound;
-  // the wide form (wgt_geom.h kW8*): 128-B records and its own triangle records, their decode
-  // step and 1 / step (the same origin bound cbound); w8 = 0 when the tree has no wide form
-  const float4* __restrict__ w8nodes;
-  const float4* __restrict__ w8tris;
-  const uint32_t* __restrict__ w8leaf;  // per group g: its records' L word (a popped triangle group's mask)
-  float w8step, rw8step;
-  uint32_t w8;
   uint32_t n_lights, n_quads, n_spheres, n_tris;
   uint32_t n_nodes;
   uint32_t last_sphere_emissive;
@@ -96,7 +88,7 @@ inline size_t ps_stack_lds_bytes(const DevScene& sc) {
 // lds_sweep_*.jsonl): 24 workgroups per CU run at full speed with 6,272 B each and lose 8-20 %
 // from 6,464 B on, although the occupancy API still reports 24 (and 160 KiB would hold 24 of
 // 6,656 B): the usable budget lies between 24 x 6,400 and 24 x 6,656 B, so 150 KiB is taken
-// (6 waves: 18 entries of 3 B beside the 11 parked words; 7 waves: 13 of 3 B; 5 waves: 19 of 4 B)
+// (6 waves: 18 entries of 3 B beside the 11 parked words; 5 waves: 19 of 4 B)
 constexpr size_t kPsLdsPerCu = 150 * 1024;
 inline uint32_t ps_cap_max(uint32_t waves) {
   const size_t per_wave = kPsLdsPerCu / (4 * waves), entry = waves >= 6 ? 3 : 4;
@@ -132,8 +124,7 @@ struct DevFrame {
   // number >= tri_ratio % of the lanes with a node to visit
   uint32_t tri_ratio;
   // BVH node form of k_render_ps: 0 = 128-B nodes, 1 = 80-B compact records, 2 = 80-B
-  // compact records when the 128-B tree exceeds kCompactNodeBytes (default), 3 = 64-B
-  // compact records (node_form)
+  // compact records when the 128-B tree exceeds kCompactNodeBytes (default) (node_form)
   uint32_t cnode;
   // persistent k_render_ps: pixel slots of the launch (64 per 8x8 block), the
   // idle lanes that trigger a refill from the pixel queue, LPT ordering (0 = off,
@@ -175,7 +166,15 @@ enum {
   CNT_STACK_SPILLS,   // parked k_render_ps: LDS stack overflows moved to the global stack
   CNT_STACK_REFILLS,  // ... and refills from it
   CNT_STACK_OVERFLOWS,  // ... and traversals park_fix ended on its overflow exit (a wrong pixel)
-  CNT_N = 24
+  // traversal phase by tree level (instrumented pass): lane visits of nodes at levels 1-2 (the
+  // root's children and grandchildren; the root itself is visited in the service phase), and the
+  // cycles of node steps, of node steps whose every visiting lane is at levels 1-2, and of
+  // triangle steps
+  CNT_TOP_NODES,
+  CNT_CYC_NODE_STEPS,
+  CNT_CYC_TOP_STEPS,
+  CNT_CYC_TRI_STEPS,
+  CNT_N = 28
 };
 
 // Launchers implemented in wgt_kernels.hip
@@ -193,7 +192,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
                          unsigned long long* counters, uint32_t resident, void* ws, size_t ws_cap,
                          hipStream_t stream, uint32_t& ws_clean_nb);
 // The node form k_render_ps reads for this scene and frame (DevFrame::cnode): 0 = 128-B
-// nodes, 1 = 80-B compact records, 2 = 64-B compact records.
+// nodes, 1 = 80-B compact records.
 int node_form(const DevScene& sc, const DevFrame& fr);
 // Waves of k_render_ps resident on the whole device for this scene's LDS stack.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves);

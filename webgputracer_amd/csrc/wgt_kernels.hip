@@ -121,9 +121,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   // noalias pointer, so its stores do not clobber the scene for the compiler, whose
   // wave-uniform loads (quads, spheres, the root node) stay scalar loads
   extern __shared__ int s_stack[];  // stack entries per lane (+ parked words), ps_stack_lds_bytes
-  // 6 or 7 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
+  // 6 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
   using STK = typename std::conditional<W >= 6, Stack24, Stack32>::type;
-  static_assert(!(PK && CN == 3), "the wide form keeps its whole stack in LDS");
   const uint32_t cap = PK ? sc.ps_cap : sc.stack;  // LDS stack entries per lane
   // PK: the highest stack top a node step may start from, cap - 4 (3 pushes and a parked
   // leaf above it); no bound when the LDS holds the builder's whole stack (cap = sc.stack),
@@ -172,6 +171,9 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   bool nanray = false;  // the pending hit is a NaN ray's (emissive last sphere), resolved at finalise
   uint64_t cyc_svc = 0, cyc_trav = 0;
   uint64_t cr_refill = 0, cr_fin = 0, cr_shade = 0, cr_cam = 0, cr_quads = 0, cr_root = 0;
+  // STATS: traversal steps by BVH level (CNT_TOP_NODES .. CNT_CYC_TRI_STEPS)
+  uint64_t cs_node = 0, cs_top = 0, cs_tri = 0;
+  uint32_t top_visits = 0;
   uint32_t pblock = 0, work = 0;  // COST: the pixel's block and its work so far
 
   for (;;) {
@@ -309,7 +311,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             }
             // (PK: a root step pushes at most 4 entries, and the LDS stack holds >= kMinPsCap
             // = 8, so the ray starts its traversal with a top <= top_max)
-            if (trav_fin<CN>(t)) pending = true;
+            if (trav_done(t)) pending = true;
             else trav = true;
           } else {
             pending = true;  // no triangles: the quad and sphere scans are the whole query
@@ -341,21 +343,24 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       // one uniform mode per step: triangle steps once enough lanes hold a
       // pending leaf (weighted by the two steps' costs), else node steps
       const bool can_node = t.ref != kNoRef;  // implies trav (invariant above)
-      const bool can_tri = CN == 3 ? w8_can_tri(t) : t.lf < t.le;  // implies trav
+      const bool can_tri = t.lf < t.le;  // implies trav
       const uint32_t nn = (uint32_t)__popcll(__ballot(can_node));
       const uint32_t nl = (uint32_t)__popcll(__ballot(can_tri));
       const bool tri_mode = nn == 0 || nl * 100u >= nn * fr.tri_ratio;
       if (STATS && (tri_mode ? can_tri : can_node)) simt_count(st.wave_steps, st.lane_steps);
       if (COST && (tri_mode ? can_tri : can_node)) ++work;
+      const uint64_t ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
+      bool all_top = false;  // STATS: every lane visiting a node this step is at level 1 or 2
+      if (STATS && !tri_mode) {
+        const bool top = can_node && sc.node_level[(uint32_t)t.ref / (CN ? kCRecordFloat4s * 16u : kNode4Floats * 4u)] <= 2u;
+        top_visits += top ? 1u : 0u;
+        all_top = __ballot(can_node && !top) == 0ull;
+      }
       if (tri_mode) {
-        if (can_tri) {
-          if constexpr (CN == 3) tri_step_w8<STATS>(sc, ro, rd, t, lds, st);
-          else tri_step<STATS, CN>(sc, ro, rd, t, lds, st);
-        }
+        if (can_tri) tri_step<STATS, CN>(sc, ro, rd, t, lds, st);
       } else {
         if (can_node) {
-          if constexpr (CN == 3) node_step_w8<STATS>(sc, t, lds, st);
-          else node_step<STATS, CN>(sc, t, lds, st);
+          node_step<STATS, CN>(sc, t, lds, st);
           // PK: fewer than 4 free LDS entries above the top (only node steps push): the
           // lane parks its state and leaves as if done; its service pass spills (park_fix)
           if (PK && (uint32_t)t.sp > top_max) {
@@ -367,7 +372,15 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           }
         }
       }
-      if (trav && trav_fin<CN>(t)) {
+      if (STATS) {
+        const uint64_t dt = __builtin_amdgcn_s_memtime() - ts0;
+        if (tri_mode) cs_tri += dt;
+        else {
+          cs_node += dt;
+          cs_top += all_top ? dt : 0u;
+        }
+      }
+      if (trav && trav_done(t)) {
         trav = false;
         pending = true;
       }
@@ -389,7 +402,11 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
       atomicAdd(&counters[CNT_CYC_CAMERA], (unsigned long long)cr_cam);
       atomicAdd(&counters[CNT_CYC_QUADS], (unsigned long long)cr_quads);
       atomicAdd(&counters[CNT_CYC_ROOT], (unsigned long long)cr_root);
+      atomicAdd(&counters[CNT_CYC_NODE_STEPS], (unsigned long long)cs_node);
+      atomicAdd(&counters[CNT_CYC_TOP_STEPS], (unsigned long long)cs_top);
+      atomicAdd(&counters[CNT_CYC_TRI_STEPS], (unsigned long long)cs_tri);
     }
+    atomicAdd(&counters[CNT_TOP_NODES], (unsigned long long)top_visits);
   }
 }
 
@@ -520,41 +537,30 @@ hipError_t launch_selftest_math(uint32_t n, uint32_t seed, unsigned long long* d
   return hipGetLastError();
 }
 
-// k_render_ps reads the compact nodes when asked to, or by default when the 128-B
-// tree would not fit one XCD's 4 MB L2 (sponza stand-in: 8.5 MB -> 4.3 + 1.1 MB);
-// a tree that fits keeps the 128-B nodes, whose step needs fewer VALU.
-// k_render_ps at the scene's waves per SIMD and node form.
+// k_render_ps at the scene's waves per SIMD (6 with 3-byte stack entries, else 5), the frame's node
+// form (node_form: 0 = 128-B nodes, 1 = 80-B compact records) and the scene's traversal state (parked
+// in LDS during service passes, or not: DevScene::ps_park).  Scenes without triangles run the
+// traversal-free instantiation.
 template <bool STATS, bool COST, int CN, int W>
 void ps_launch_w(const DevScene& sc, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
                  const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
                  uint32_t* queue) {
-  if constexpr (CN == 3)  // the wide form: the whole stack in LDS (node_form never picks it parked)
-    k_render_ps<STATS, COST, 3, W, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
-  else if (sc.ps_park)
+  if (sc.ps_park)
     k_render_ps<STATS, COST, CN, W, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
   else
     k_render_ps<STATS, COST, CN, W, true, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
 }
-// k_render_ps at the scene's waves per SIMD and the frame's node form (node_form); the
-// 64-B form is instantiated at 6 waves only (its 24-bit refs are those of Stack24 trees)
 template <bool STATS, bool COST>
 void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hipStream_t stream, const DevFrame& f,
                const wgt_tile* tiles, uchar4* out8, float4* out32, uint32_t* outhit, unsigned long long* counters,
                uint32_t* queue) {
   if (sc.n_tris == 0) {
     k_render_ps<STATS, COST, 0, kPsWavesNoTris, false><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
-  } else if (sc.ps_waves == 7) {  // parked state only (the whole stack does not fit LDS at 7)
-    if (cn == 2) k_render_ps<STATS, COST, 2, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
-    else if (cn == 1) k_render_ps<STATS, COST, 1, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
-    else k_render_ps<STATS, COST, 0, 7, true, true><<<grid, block, lds, stream>>>(sc, f, tiles, out8, out32, outhit, counters, queue, f.ps_spill);
   } else if (sc.ps_waves == 6) {
-    if (cn == 3) ps_launch_w<STATS, COST, 3, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
-    else if (cn == 2) ps_launch_w<STATS, COST, 2, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
-    else if (cn == 1) ps_launch_w<STATS, COST, 1, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    if (cn) ps_launch_w<STATS, COST, 1, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
     else ps_launch_w<STATS, COST, 0, 6>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
   } else {
-    if (cn == 3) ps_launch_w<STATS, COST, 3, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
-    else if (cn) ps_launch_w<STATS, COST, 1, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
+    if (cn) ps_launch_w<STATS, COST, 1, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
     else ps_launch_w<STATS, COST, 0, 5>(sc, grid, block, lds, stream, f, tiles, out8, out32, outhit, counters, queue);
   }
 }
@@ -562,20 +568,13 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
 // The compact codes are exact for ray origins within their bound (the margin, wgt_geom.h):
 // hit points always are, the camera is checked per frame (beyond: the 128-B nodes).
 // WGT_CNODE: 0 = 128-B, 1 = 80-B, 2 = 80-B when the 128-B tree would not fit one XCD's
-// 4 MB L2 (sponza stand-in: 7.3 MB -> 4.6 MB; default), 3 = 64-B (at 6 waves per SIMD, when
-// the tree fits the form; else as 1).  A tree that fits keeps the 128-B nodes, whose step
-// needs fewer VALU.
-// 4 = the wide 8-slot records (when the scene has them and the traversal state is not parked; else as
-// 2: the scene was uploaded without WGT_CNODE=4 or WGT_W8=1, host/bvh.cpp WideWanted).
+// 4 MB L2 (sponza stand-in: 7.3 MB -> 4.6 MB; default).  A tree that fits keeps the 128-B nodes,
+// whose step needs fewer VALU.  (Round 6 removed the 64-B records, WGT_CNODE=3,
+// and the wide 8-slot records, WGT_CNODE=4: slower on every measured scene)
 int node_form(const DevScene& sc, const DevFrame& fr) {
   const float cam = fmaxf(fmaxf(fabsf(fr.ox), fabsf(fr.oy)), fabsf(fr.oz));
-  if (fr.cnode == 4 && sc.w8 && !sc.ps_park && sc.ps_waves <= 6 && cam <= sc.cbound) return 3;
-  if (fr.cnode == 3 && sc.ps_waves >= 6 && cam <= sc.c64bound) return 2;
   if (!(cam <= sc.cbound)) return 0;
-  return fr.cnode == 1 || fr.cnode == 3 ||
-                 ((fr.cnode == 2 || fr.cnode == 4) && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes)
-             ? 1
-             : 0;
+  return fr.cnode == 1 || (fr.cnode >= 2 && (size_t)sc.n_nodes * kNode4Floats * 4 > kCompactNodeBytes) ? 1 : 0;
 }
 
 // the parked kernel's global stacks: sc.stack entries per lane of every resident wave
@@ -661,22 +660,14 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   return hipGetLastError();
 }
 
-// k_render_ps<STATS = false, COST = false, CN, W> of a launchable form
+// k_render_ps<STATS = false, COST = false, CN, W, true, PK> of a launchable form
 template <int W, bool PK>
 const void* ps_kernel(int cn) {
-  if constexpr (W == 7) {
-    return cn == 2 ? reinterpret_cast<const void*>(&k_render_ps<false, false, 2, 7, true, true>)
-                   : cn == 1 ? reinterpret_cast<const void*>(&k_render_ps<false, false, 1, 7, true, true>)
-                             : reinterpret_cast<const void*>(&k_render_ps<false, false, 0, 7, true, true>);
-  } else {
-    if (cn == 3) return reinterpret_cast<const void*>(&k_render_ps<false, false, 3, W, true, false>);
-    if (cn == 2 && W == 6) return reinterpret_cast<const void*>(&k_render_ps<false, false, (W == 6 ? 2 : 1), W, true, PK>);
-    return cn ? reinterpret_cast<const void*>(&k_render_ps<false, false, 1, W, true, PK>)
-              : reinterpret_cast<const void*>(&k_render_ps<false, false, 0, W, true, PK>);
-  }
+  return cn ? reinterpret_cast<const void*>(&k_render_ps<false, false, 1, W, true, PK>)
+            : reinterpret_cast<const void*>(&k_render_ps<false, false, 0, W, true, PK>);
 }
 
-// The persistent grid: the smallest resident capacity over the node forms the scene's launches can
+// The persistent grid: the smaller resident capacity of the two node forms the scene's launches can
 // read (node_form), so that every wave of a launch is resident from its start.
 hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
   int per_cu = 0, cus = 0;
@@ -687,12 +678,9 @@ hipError_t ps_resident_waves(const DevScene& sc, int device, uint32_t& waves) {
     if (e != hipSuccess) return e;
   } else {
     per_cu = 1 << 30;
-    for (int cn = 0; cn < 4; ++cn) {
-      if (cn == 2 && !(sc.ps_waves >= 6 && sc.c64bound >= 0.0f)) continue;
-      if (cn == 3 && !(sc.w8 && !sc.ps_park && sc.ps_waves <= 6)) continue;
-      const void* k = sc.ps_waves == 7 ? ps_kernel<7, true>(cn)
-                      : sc.ps_waves == 6 ? (sc.ps_park ? ps_kernel<6, true>(cn) : ps_kernel<6, false>(cn))
-                                         : (sc.ps_park ? ps_kernel<5, true>(cn) : ps_kernel<5, false>(cn));
+    for (int cn = 0; cn < 2; ++cn) {
+      const void* k = sc.ps_waves == 6 ? (sc.ps_park ? ps_kernel<6, true>(cn) : ps_kernel<6, false>(cn))
+                                       : (sc.ps_park ? ps_kernel<5, true>(cn) : ps_kernel<5, false>(cn));
       int n = 0;
       const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k, kBlock, ps_stack_lds_bytes(sc));
       if (e != hipSuccess) return e;

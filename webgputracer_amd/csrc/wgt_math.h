@@ -106,6 +106,37 @@ WGT_HD float div_rn(float n, float d) {
   return n / d;
 #endif
 }
+// Division by a shared denominator: the reciprocal refined once (rcp_of), then per
+// numerator div_rn's two residual corrections and v_div_fixup (div_by), which sets the
+// sign, zeros, infinities and NaNs as the IEEE sequence does.  Without v_div_scale the
+// result is the IEEE quotient when the operands are in the unscaled domain (wgt_math.h
+// div_safe); callers take it only under that guard.
+struct RcpF {
+  float d, r;
+};
+WGT_HD RcpF rcp_of(float d) {
+#ifdef __HIP_DEVICE_COMPILE__
+  float r = __builtin_amdgcn_rcpf(d);
+  r = __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+  return RcpF{d, r};
+#else
+  return RcpF{d, 0.0f};
+#endif
+}
+WGT_HD float div_by(float n, RcpF R) {
+#ifdef __HIP_DEVICE_COMPILE__
+  float q = n * R.r;
+  q = __builtin_fmaf(__builtin_fmaf(-R.d, q, n), R.r, q);
+  q = __builtin_fmaf(__builtin_fmaf(-R.d, q, n), R.r, q);
+  return __builtin_amdgcn_div_fixupf(q, R.d, n);
+#else
+  return n / R.d;
+#endif
+}
+WGT_HD f3 div3_by(f3 a, float s) {
+  const RcpF R = rcp_of(s);
+  return f3{div_by(a.x, R), div_by(a.y, R), div_by(a.z, R)};
+}
 WGT_HD float length(f3 a) { return sqrt_rn(dot(a, a)); }
 // WGSL normalize(v) = v / length(v)   (zero vector -> NaN, as the reference relies on)
 WGT_HD f3 normalize(f3 a) { return a / length(a); }

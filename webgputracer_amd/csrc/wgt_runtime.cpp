@@ -151,24 +151,9 @@ uint32_t ps_waves_for(const BvhOut& bvh, uint32_t n_tris) {
   // no triangles: the kernel without traversal (4-byte stack bytes in the launch and
   // the occupancy query alike, ps_stack_lds_bytes)
   if (n_tris == 0) return (uint32_t)kPsWavesNoTris;
-  const uint32_t forced = env_u32("WGT_PS_WAVES", 0);
-  if (forced == 5) return 5u;
+  if (env_u32("WGT_PS_WAVES", 0) == 5) return 5u;
   const bool fits24 = bvh.n_nodes < kStack24Nodes && n_tris < kStack24Tris;
-  // 7 waves per SIMD (72 VGPRs) exist with the parked state only (WGT_PS_WAVES=7 parks)
-  if (forced == 7 && fits24) return 7u;
   return fits24 ? 6u : 5u;
-}
-
-// Whether the tree has the 64-B compact form (wgt_geom.h kC64RecordFloat4s): every node's
-// origin fits its grid byte (c64_ok) and every child ref its 24-bit field (internal refs
-// as byte offsets of 64-B records, leaf refs as they are).
-bool c64_fits(const BvhOut& bvh) {
-  if (!bvh.c64_ok || bvh.n_nodes == 0) return false;
-  for (int32_t r : bvh.crefs) {
-    const int64_t b = r >= 0 ? (int64_t)r * kC64RecordFloat4s * 16 : (int64_t)r;
-    if (b >= (1 << 23) || b < -(1 << 23)) return false;
-  }
-  return true;
 }
 
 // Parked traversal state of k_render_ps (opt-in: WGT_PARK=1; it
@@ -176,27 +161,13 @@ bool c64_fits(const BvhOut& bvh) {
 // stack holds what fits beside the parked words at the wave budget,
 // or the whole stack (`stack` entries) when that is smaller; WGT_PS_CAP lowers it, down to
 // kMinPsCap, for tests.
-// 7 waves per SIMD park (the only form of that budget); a WGT_PS_WAVES=7 request that the tree cannot
-// take (ps_waves_for gave 6 or 5) does not park unless WGT_PARK asks for it.
 void ps_park_cap(uint32_t n_tris, uint32_t stack, uint32_t waves, uint32_t& park, uint32_t& cap) {
-  park = n_tris > 0 && (env_u32("WGT_PARK", 0) || waves == 7) ? 1u : 0u;
+  park = n_tris > 0 && env_u32("WGT_PARK", 0) ? 1u : 0u;
   cap = stack;
   if (!park) return;
   uint32_t c = std::min(stack, ps_cap_max(waves));
   c = std::min(c, std::max(env_u32("WGT_PS_CAP", c), kMinPsCap));
   cap = std::max(c, kMinPsCap);
-}
-
-// The wide form's figures in wgt_scene_info (usable: the scene's launches can read it).
-void fill_w8_info(const BvhOut& bvh, bool usable, wgt_scene_info& in) {
-  in.bvh_w8 = usable ? 1u : 0u;
-  in.w8_groups = bvh.w8_groups;
-  in.w8_nodes = bvh.w8_nodes;
-  in.w8_leaves = bvh.w8_leaves;
-  in.w8_depth = bvh.w8_depth;
-  in.w8_stack = bvh.w8_stack;
-  in.w8_step = bvh.w8step;
-  in.w8_sah = bvh.w8_sah;
 }
 
 DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
@@ -367,6 +338,10 @@ void fill_stats(const unsigned long long* c, wgt_stats* s) {
   s->stack_spills = c[CNT_STACK_SPILLS];
   s->stack_refills = c[CNT_STACK_REFILLS];
   s->stack_overflows = c[CNT_STACK_OVERFLOWS];
+  s->top_node_visits = c[CNT_TOP_NODES];
+  s->cyc_node_steps = c[CNT_CYC_NODE_STEPS];
+  s->cyc_top_steps = c[CNT_CYC_TOP_STEPS];
+  s->cyc_tri_steps = c[CNT_CYC_TRI_STEPS];
 }
 
 
@@ -407,8 +382,11 @@ int render_frame(wgt_ctx* ctx, const DevFrame& fr, const wgt_tile* d_tiles, ucha
   const size_t ws_need = render_ws_bytes(ctx->sc, fr, ctx->ps_resident);
   if (sl.ws.bytes < ws_need && (rc = use_drain(ctx))) return rc;  // before regrowing
   const void* old_ws = sl.ws.p;
+  const size_t old_bytes = sl.ws.bytes;
   if ((rc = ensure(ctx, sl.ws, ws_need))) return rc;
-  if (sl.ws.p != old_ws) sl.clean_nb = 0;  // a new workspace: nothing is known zero
+  // a new workspace (ensure reallocated: its size changed, whatever address hipMalloc returned):
+  // nothing is known zero
+  if (sl.ws.p != old_ws || sl.ws.bytes != old_bytes) sl.clean_nb = 0;
   if (!sl.ev) WGT_HIP(ctx, hipEventCreateWithFlags(&sl.ev, hipEventDisableTiming));
   else WGT_HIP(ctx, hipStreamWaitEvent(s, sl.ev, 0));
   {
@@ -560,38 +538,8 @@ int wgt_bvh_build(const wgt_triangle* tris, uint32_t n_tris, float* nodes_out, u
   info->bvh_compact = (size_t)bvh.n_nodes * kNode4Floats * 4 > kCompactNodeBytes ? 1u : 0u;
   info->bvh_compact_step = bvh.cstep;
   info->ps_waves = ps_waves_for(bvh, n_tris);
-  info->bvh_c64 = c64_fits(bvh) ? 1u : 0u;
   ps_park_cap(n_tris, (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u, info->ps_waves, info->ps_park,
               info->ps_stack);
-  fill_w8_info(bvh, bvh.w8_ok, *info);
-  return WGT_OK;
-}
-
-int wgt_bvh_build_wide(const wgt_triangle* tris, uint32_t n_tris, uint32_t* recs_out, uint32_t recs_cap,
-                       float* tris_out, uint32_t tri_recs_cap, wgt_scene_info* info) {
-  if (!tris || n_tris == 0 || !info) return fail(nullptr, WGT_E_INVALID, "null triangles or info");
-  BvhOut bvh;
-  bvh.want_wide = true;
-  std::string err;
-  if (!BuildBvh(tris, n_tris, (uint32_t)kMaxBvhDepth, stack_limit(), narrow_limit(), narrow_ratio(),
-                kOriginBoundScale * scene_extent(nullptr, 0, nullptr, 0, tris, n_tris), bvh, err))
-    return fail(nullptr, WGT_E_INVALID, err);
-  if (!bvh.w8_ok) return fail(nullptr, WGT_E_INVALID, "the tree has no wide form");
-  *info = wgt_scene_info{};
-  info->n_tris = n_tris;
-  info->bvh_compact_step = bvh.cstep;
-  fill_w8_info(bvh, true, *info);
-  info->w8_records = (uint32_t)(bvh.w8nodes.size() / kW8RecordWords);
-  info->w8_bound = bvh.cbound;
-  if (recs_out) {
-    if (recs_cap < info->w8_records) return fail(nullptr, WGT_E_INVALID, "record capacity too small");
-    std::memcpy(recs_out, bvh.w8nodes.data(), bvh.w8nodes.size() * 4);
-  }
-  if (tris_out) {
-    if ((size_t)tri_recs_cap * kTriRecordFloats < bvh.w8tris.size())
-      return fail(nullptr, WGT_E_INVALID, "triangle record capacity too small");
-    std::memcpy(tris_out, bvh.w8tris.data(), bvh.w8tris.size() * 4);
-  }
   return WGT_OK;
 }
 
@@ -649,20 +597,6 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     std::memcpy(&crec[i * kCRecordFloat4s * 4], &bvh.cnodes[i * kCNodeFloats], kCNodeFloats * 4);
     std::memcpy(&crec[i * kCRecordFloat4s * 4 + kCNodeFloats], &bvh.crefs[i * 4], 16);
   }
-  // the 64-B form (WGT_CNODE=3): codes, then 24-bit refs (internal: byte offsets) under the
-  // origin bytes; a tree whose refs or origins do not fit it has none (c64 = false)
-  bool c64 = c64_fits(bvh);
-  std::vector<uint32_t> c64rec(c64 ? (size_t)bvh.n_nodes * kC64RecordFloat4s * 4 : 0);
-  for (size_t i = 0; c64 && i < bvh.n_nodes; ++i) {
-    std::memcpy(&c64rec[i * 16], &bvh.c64[i * 16], 64);
-    for (int k = 0; k < 4; ++k) {
-      int64_t r = bvh.crefs[i * 4 + k];
-      if (r >= 0) r *= kC64RecordFloat4s * 16;
-      if (r >= (1 << 23) || r < -(1 << 23)) c64 = false;
-      c64rec[i * 16 + 12 + k] |= (uint32_t)r & 0xffffffu;
-    }
-  }
-  if (!c64) c64rec.clear();
   // device copies address child nodes by byte offset (one add to the uniform base in
   // the kernels instead of an index multiply); leaf refs are unchanged
   for (size_t i = 0; i < bvh.n_nodes; ++i)
@@ -675,6 +609,15 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
       std::memcpy(&bvh.nodes[i * kNode4Floats + 24 + k], &r128, 4);
     }
   const size_t b_cnodes = align256(crec.size() * 4);
+  // each node's level (root 0, saturating at 255): preorder refs point forward, so one pass
+  std::vector<uint8_t> level(bvh.n_nodes, 0);
+  for (size_t i = 0; i < bvh.n_nodes; ++i)
+    for (int k = 0; k < 4; ++k) {
+      int32_t r;
+      std::memcpy(&r, &bvh.crefs[i * 4 + k], 4);
+      if (r >= 0 && (size_t)r < bvh.n_nodes) level[r] = (uint8_t)std::min(255, level[i] + 1);
+    }
+  const size_t b_level = align256(level.size());
   // the device triangle records (wgt_geom.h kTriRecordBytes): the builder's 64-B records,
   // or their 40-B form without the padded box
   std::vector<float> dtris;
@@ -692,16 +635,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   }
   const size_t b_tris = align256(dtris.size() * 4);
   const size_t b_shade = align256(bvh.tshade.size() * 4);
-  const size_t b_c64 = align256(c64rec.size() * 4);
-  // the wide form (wgt_geom.h kW8*): its records and triangle records; Stack24 entries hold a
-  // 15-bit group index (6 waves per SIMD), Stack32 ones 23 bits
   const uint32_t waves = ps_waves_for(bvh, n_tris);
-  const bool w8 = n_tris > 0 && bvh.w8_ok && bvh.w8_stack <= (uint32_t)kStackMax + 1u &&
-                  bvh.w8_groups < (waves >= 6 ? (1u << 15) : (1u << 23));
-  const size_t b_w8 = w8 ? align256(bvh.w8nodes.size() * 4) : 0;
-  const size_t b_w8t = w8 ? align256(bvh.w8tris.size() * 4) : 0;
-  const size_t b_w8l = w8 ? align256(bvh.w8leaf.size() * 4) : 0;
-  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64 + b_w8 + b_w8t + b_w8l;
+  const size_t total = b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_level;
 
   {
     int rc = use_drain(ctx);  // no launch on any stream may still read the old scene
@@ -712,6 +647,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     ctx->scene_mem = nullptr;
   }
   ctx->has_scene = false;
+  // a new scene: the workspaces' scheduling words are re-zeroed by the next launch's memset
+  for (auto& sl : ctx->slots) sl.clean_nb = 0;
   WGT_HIP(ctx, hipMalloc(&ctx->scene_mem, total));
   char* base = (char*)ctx->scene_mem;
   std::vector<char> host(total, 0);
@@ -724,15 +661,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris, bvh.tshade.data(),
                 bvh.tshade.size() * 4);
     std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade, crec.data(), crec.size() * 4);
-    if (c64)
-      std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes, c64rec.data(),
-                  c64rec.size() * 4);
-    if (w8) {
-      char* w8base = host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64;
-      std::memcpy(w8base, bvh.w8nodes.data(), bvh.w8nodes.size() * 4);
-      std::memcpy(w8base + b_w8, bvh.w8tris.data(), bvh.w8tris.size() * 4);
-      std::memcpy(w8base + b_w8 + b_w8t, bvh.w8leaf.data(), bvh.w8leaf.size() * 4);
-    }
+    std::memcpy(host.data() + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes, level.data(), level.size());
   }
   WGT_HIP(ctx, hipMemcpy(base, host.data(), total, hipMemcpyHostToDevice));
 
@@ -744,18 +673,9 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.tris = (const float4*)(base + b_quads + b_sph + b_nodes);
   sc.tshade = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris);
   sc.cnodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade);
-  sc.cnodes64 = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes);
-  sc.w8nodes = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64);
-  sc.w8tris = (const float4*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64 + b_w8);
-  sc.w8leaf = (const uint32_t*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes + b_c64 + b_w8 + b_w8t);
-  sc.w8 = w8 ? 1u : 0u;
-  sc.w8step = bvh.w8step;
-  sc.rw8step = 1.0f / bvh.w8step;  // a power of two: exact
+  sc.node_level = (const uint8_t*)(base + b_quads + b_sph + b_nodes + b_tris + b_shade + b_cnodes);
   sc.cstep = bvh.cstep;
   sc.cbound = bvh.cbound;
-  sc.c64step = bvh.c64step;
-  sc.rc64step = 1.0f / sc.c64step;  // a power of two: exact
-  sc.c64bound = c64 ? bvh.cbound : -1.0f;  // without the 64-B form, WGT_CNODE=3 reads the 80-B one
   sc.rcstep = 1.0f / sc.cstep;  // a power of two: exact
   sc.n_lights = n_lights;
   sc.n_quads = n_quads;
@@ -768,11 +688,7 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
   // + 1: the speculative traversal parks a second leaf on the stack (wgt_device.h)
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
-  if (w8) sc.stack = std::max(sc.stack, bvh.w8_stack);  // the wide traversal's groups: 2 per level
   sc.ps_waves = waves;
-  if (env_u32("WGT_PS_WAVES", 0) == 7 && waves != 7 && env_u32("WGT_DEBUG", 0))
-    std::fprintf(stderr, "[wgt] WGT_PS_WAVES=7: the tree's refs do not fit 3-byte stack entries; %u waves per SIMD\n",
-                 waves);
   // parked traversal state (WGT_PARK=0: the whole stack in LDS);
   // the LDS stack holds what fits beside the parked words at the wave budget, or the whole
   // stack when that is smaller (WGT_PS_CAP lowers it, down to kMinPsCap, for tests)
@@ -803,8 +719,6 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   in.ps_waves = n_tris ? sc.ps_waves : 0u;
   in.ps_park = sc.ps_park;
   in.ps_stack = n_tris ? sc.ps_cap : 0u;
-  in.bvh_c64 = c64 ? 1u : 0u;
-  fill_w8_info(bvh, w8, in);
   {
     const wgt_camera_param cam{{278.0f, 278.0f, -800.0f}, 0.0f, {278.0f, 278.0f, 0.0f}, 0.0f, 1.0f, 40.0f, 1u, 0u};
     in.node_form = n_tris ? (uint32_t)node_form(sc, make_frame(cam, 1, 1)) : 0u;

@@ -234,7 +234,13 @@ class ShardedFrames:
     def gather(self, slot=0):
         """Gather every rank's tiles of buffer set `slot` to rank 0 and assemble (on torch's current
         stream, which must be the one the launch ran on): {kind: {frame id: (H, W, 4) tensor}} on
-        rank 0, None elsewhere."""
+        rank 0, None elsewhere.
+
+        Lifetime: when one rank renders whole frames (`whole`, N = 1 without a collective) the
+        tensors are VIEWS of buffer set `slot` (no copy), valid until the set is launched again;
+        otherwise they are assembled copies.  A caller that keeps a frame past the set's next
+        launch clones it first (wait_slot orders that launch after the gather only, not after
+        the caller's reads)."""
         import torch
 
         out = {}

@@ -110,20 +110,6 @@ def bvh_build_compact(tris):
     return cn, cr, step.value
 
 
-def bvh_build_wide(tris):
-    """Host-only wide form of the scene's triangles (wgt_bvh_build_wide, wgt_geom.h kW8*):
-    (info, records (w8_records, 32) u32, triangle records (4 * w8_records, 4, 4) f32)."""
-    tris = np.ascontiguousarray(tris, TRI_DTYPE)
-    L = lib()
-    info = WgtSceneInfo()
-    check(L.wgt_bvh_build_wide(ptr(tris), len(tris), None, 0, None, 0, ctypes.byref(info)))
-    n = info.w8_records
-    recs = np.zeros((n, 32), np.uint32)
-    trec = np.zeros((4 * n, 4, 4), np.float32)
-    check(L.wgt_bvh_build_wide(ptr(tris), len(tris), ptr(recs), n, ptr(trec), 4 * n, ctypes.byref(info)))
-    return info.as_dict(), recs, trec
-
-
 def camera_param(aspect: float, spp: int, seed: int, fovy: float = 40.0):
     """Camera::Update (camera.cpp:64-70) with an explicit seed instead of RandSeed()."""
     cam = np.zeros(1, CAMERA_DTYPE)
