@@ -131,6 +131,9 @@ typedef struct {
    * tested in the service phase), wave cycles of node steps, of the node steps whose visiting lanes
    * are all at levels 1-2 (what an LDS copy of the top levels could shorten), and of triangle steps */
   uint64_t top_node_visits, cyc_node_steps, cyc_top_steps, cyc_tri_steps;
+  /* rays whose quad scan took the reference path with per-quad distances (an almost-tie in
+   * distance between two quads) */
+  uint64_t quad_ref_scans;
 } wgt_stats;
 
 typedef struct {

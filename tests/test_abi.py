@@ -44,8 +44,8 @@ def test_struct_sizes_match_reference_layouts(wgt):
     assert _lib.SPHERE_DTYPE.itemsize == 32    # scene.h:47 sphere_stride_
     assert _lib.TRI_DTYPE.itemsize == 80       # scene.h:45 tri_stride_
     assert _lib.CAMERA_DTYPE.itemsize == 48    # camera.h:19-31
-    # + stack_spills, stack_refills (round 4), stack_overflows (5), the four by-level traversal figures (6)
-    assert ctypes.sizeof(_lib.WgtStats) == 224
+    # + stack_spills, stack_refills (round 4), stack_overflows (5), the four by-level traversal figures and quad_ref_scans (6)
+    assert ctypes.sizeof(_lib.WgtStats) == 232
 
 
 def test_ctypes_structs_match_the_header(tmp_path):

@@ -44,7 +44,8 @@ class WgtStats(ctypes.Structure):
                 ("cyc_root", ctypes.c_uint64), ("stack_spills", ctypes.c_uint64),
                 ("stack_refills", ctypes.c_uint64), ("stack_overflows", ctypes.c_uint64),
                 ("top_node_visits", ctypes.c_uint64), ("cyc_node_steps", ctypes.c_uint64),
-                ("cyc_top_steps", ctypes.c_uint64), ("cyc_tri_steps", ctypes.c_uint64)]
+                ("cyc_top_steps", ctypes.c_uint64), ("cyc_tri_steps", ctypes.c_uint64),
+                ("quad_ref_scans", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

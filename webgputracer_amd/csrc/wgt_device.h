@@ -124,6 +124,71 @@ __device__ __forceinline__ void quad_scan(const DevScene& sc, f3 o, f3 d, Hit& h
   }
 }
 
+// The quad scan of the persistent kernel: quad_scan's result (the accepted quad and its t) without
+// the per-quad distance and its square root ("quad distance").
+//
+// quad_scan accepts quad k when it is valid (t in range, inside the quad) and its rounded distance
+// f(t_k) = distance(o + t_k d, o) is below the best so far (kRayMax at first), so it returns the FIRST
+// quad (scan order) whose f equals the minimum of f over the valid quads, provided that minimum is
+// below kRayMax.  f is non-decreasing in t (every rounded step is), so the valid quad of smallest t
+// (first on equal t) attains the minimum; this scan tracks that quad (t < qt, no distance) and the
+// t of the best it replaced, `prev`: the smallest t of the valid quads before it in scan order.  Its
+// answer is quad_scan's unless f(prev) == f(t) (an earlier quad ties in distance) or f(t) >= kRayMax.
+// Both are excluded by a test on the max norms D = max|d_i|, L = max|o_i| (|.| <= ||.|| <= sqrt(3) |.|):
+//   * f(t) < kRayMax when t D < 2^64: f(t) <= (sqrt(3) t D (1 + 3 eps) + eps sqrt(3) L)(1 + 2.6 eps)
+//     + 2^-74 < 1e20 (eps = 2^-24, L < 2^41 under the scene limits);
+//   * f(t) < f(prev) when g = (prev - t) - 2^-19 (prev + t) > 0, g D > 2^-18 L and prev D >= 2^-49: each
+//     component of pos - o is t d_i within eps (3 |t d_i| + |o_i|), so ||pos - o|| is t ||d|| within
+//     eps (3 t ||d|| + ||o||); the test (computed in fp32, whose roundings its factor-2 margins absorb)
+//     gives (prev - t) ||d|| - 2^-20 (prev + t) ||d|| > 2^-19 ||o||, so the two exact norms differ by
+//     >= 2^-21 prev ||d||, more than the dot product's and square root's roundings (2.6 eps relative,
+//     2^-74 absolute from denormal squares) can close when prev ||d|| >= 2^-50.
+// A lane that fails the test (an almost-tie: rays near the line where two quads meet) takes the
+// reference scan, quad_scan; returns false for such a lane.  EXACT: as quad_scan<EXACT>.
+template <bool EXACT = false>
+__device__ __forceinline__ bool quad_scan_fast(const DevScene& sc, f3 o, f3 d, uint32_t& prim, float& qt) {
+  prim = kNoHit;
+  qt = __builtin_inff();
+  float prev = __builtin_inff();
+  const uint32_t nlq = sc.n_lights + sc.n_quads;
+  for (uint32_t k = 0; k < nlq; ++k) {
+    const float4* __restrict__ q = sc.quads + 6 * k;
+    const f3 qn = xyz(q[3]);
+    const float denom = dot(qn, d);
+    if (fabs_w(denom) < kRayMin) continue;
+    const float4 wd = q[4];
+    const float num = wd.w - dot(qn, o);
+    const float t = EXACT ? num / denom : div_rn(num, denom);
+    if (t < kRayMin || kRayMax < t) continue;
+    if (t >= qt) continue;
+    const f3 pos = o + t * d;
+    const f3 hit_vec = pos - xyz(q[0]);
+    const f3 w = xyz(wd);
+    const float a = dot(w, cross(hit_vec, xyz(q[2])));
+    const float b = dot(w, cross(xyz(q[1]), hit_vec));
+    if ((__builtin_fminf(a, b) < 0.0f) || (1.0f < __builtin_fmaxf(a, b))) continue;
+    prev = qt;
+    qt = t;
+    prim = k;
+  }
+  bool exact = true;
+  if (prim != kNoHit) {
+    const float D = __builtin_fmaxf(__builtin_fmaxf(fabs_w(d.x), fabs_w(d.y)), fabs_w(d.z));
+    const float L = __builtin_fmaxf(__builtin_fmaxf(fabs_w(o.x), fabs_w(o.y)), fabs_w(o.z));
+    exact = qt * D < 0x1p64f;
+    if (prev != __builtin_inff()) {
+      const float g = (prev - qt) - 0x1p-19f * (prev + qt);
+      exact = exact && g * D > 0x1p-18f * L && prev * D >= 0x1p-49f;
+    }
+  }
+  if (!exact) {
+    Hit h;
+    quad_scan<EXACT>(sc, o, d, h, qt);
+    prim = h.prim;
+  }
+  return exact;
+}
+
 // The quad part of a hit rebuilt from (prim, t): the same operations as isect_quad.
 __device__ __forceinline__ void quad_rebuild(const DevScene& sc, f3 o, f3 d, uint32_t prim, float t,
                                              Hit& h) {
@@ -209,9 +274,11 @@ __device__ __forceinline__ bool trav_found(const Trav& t) { return t.bi != kNoHi
 // CN (compact nodes): t.inv holds s/d (s = the form's step, a power of two: exact), the
 // factor of the fused slab step (cchild_key); the triangle box check multiplies
 // it back by 1/s.
-template <int CN = 0>
+// EXACT: the IEEE 1/d (k_trace's caller-supplied rays); else the short reciprocal (render rays).
+template <int CN = 0, bool EXACT = false>
 __device__ __forceinline__ void trav_init(const DevScene& sc, f3 o, f3 d, bool quad_hit, float qt, Trav& t) {
-  t.inv = f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)};
+  t.inv = EXACT ? f3{safe_inv(d.x), safe_inv(d.y), safe_inv(d.z)}
+                : f3{safe_inv_short(d.x), safe_inv_short(d.y), safe_inv_short(d.z)};
   t.ot = slab_offset(o, t.inv);
   if (CN) t.inv = sc.cstep * t.inv;
   // a triangle must satisfy t < t_quad to beat a quad hit (ray_dist is monotone in
@@ -415,6 +482,30 @@ struct Stack24S {
 };
 using Stack32 = Stack32S<>;
 using Stack24 = Stack24S<>;
+// Stack24 at a fixed layout (k_render_ps at 6 waves per SIMD without parked state): kStackMax + 1
+// entries per lane whatever the tree needs, the 16-bit array at LDS byte 0 and the 8-bit one at
+// kStack24HiOffset, so that entry i of lane l is addressed from one per-lane register, the lane
+// index: ((i << 6) + l) * 2 and ((i << 6) + l) + kStack24HiOffset, the offset an immediate of the
+// LDS instruction.  The pointer-pair form (Stack24) keeps two per-lane addresses live through the
+// whole kernel, which the service code's register pressure spills.
+constexpr uint32_t kStack24Entries = kStackMax + 1;
+constexpr uint32_t kStack24HiOffset = kStack24Entries * kBlock * 2;
+struct Stack24C {
+  uint32_t lane;
+  __device__ __forceinline__ int ld(int i) const {
+    const uint32_t a = ((uint32_t)i << 6) + lane;
+    extern __shared__ int s_stack[];
+    const char* b = (const char*)s_stack;
+    return ((int)*(const int8_t*)(b + kStack24HiOffset + a) << 16) | (int)*(const uint16_t*)(b + 2 * a);
+  }
+  __device__ __forceinline__ void st(int i, int v) const {
+    const uint32_t a = ((uint32_t)i << 6) + lane;
+    extern __shared__ int s_stack[];
+    char* b = (char*)s_stack;
+    *(uint16_t*)(b + 2 * a) = (uint16_t)v;
+    *(int8_t*)(b + kStack24HiOffset + a) = (int8_t)(v >> 16);
+  }
+};
 
 // Parked traversal state of k_render_ps (DevScene::ps_park): the
 // lane's Trav lives in LDS words (stride kBlock, conflict-free) while its wave runs a
@@ -662,9 +753,11 @@ __device__ __forceinline__ void sample_hit(const DevScene& sc, f3 o, f3 d, int* 
     return;
   }
   float qt;
-  quad_scan<EXACT>(sc, o, d, h, qt);
+  uint32_t qprim;
+  quad_scan_fast<EXACT>(sc, o, d, qprim, qt);
+  quad_rebuild(sc, o, d, qprim, qt, h);
   Trav t;
-  trav_init(sc, o, d, h.prim != kNoHit, qt, t);
+  trav_init<0, EXACT>(sc, o, d, h.prim != kNoHit, qt, t);
   if (TRIS) {
     while (!trav_step<STATS>(sc, o, d, t, lds, st)) {
     }
@@ -676,6 +769,11 @@ struct Light {
   f3 pos, right, up;
 };
 
+// shade's short divisions (A/B builds): bit 0 the normal's normalisations, bit 1 the sampled
+// direction's (and the light pdf)
+#ifndef WGT_SHADE_SHORT
+#define WGT_SHADE_SHORT 0
+#endif
 // raytrace() after sample_hit (path_tracer.wgsl:267-287).  Returns path.end.
 __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const Hit& h, int depth,
                                       uint32_t& seed, f3& ro, f3& rd, f3& pc) {
@@ -688,13 +786,15 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
     }
     return true;
   }
-#ifdef WGT_FASTDIV_PROBE
-  // PROBE ONLY (not exact outside the unscaled domain): the upper bound of the short forms
-  const f3 w = div3_by(h.norm, length(h.norm));
-#else
-  // sample_direction (path_tracer.wgsl:146-154)
-  const f3 w = normalize(h.norm);  // onb.w of build_onb_from_w(hit.norm)
-#endif
+  // sample_direction (path_tracer.wgsl:146-154); onb.w of build_onb_from_w(hit.norm).  Short
+  // divisions (div3_by) where they are the IEEE quotient ("shading divisions"):
+  // the scene's quad and triangle normals are unit within 2^-10 with no component below 2^-60 in
+  // magnitude but 0 (sc.fast_shade, checked at upload), so |n_i| / |n| is 0 or >= 2^-61 with |n|
+  // in [1/2, 2]; a sphere's normal is computed per hit and takes the IEEE division.
+  const bool fast_w = (WGT_SHADE_SHORT & 1) && sc.fast_shade && h.prim < sc.first_sphere;
+  f3 w;
+  if (fast_w) w = div3_by(h.norm, length(h.norm));
+  else w = normalize(h.norm);
   f3 sdir;
   // both branches draw two more rand() (r1 then r2) right away: drawn once here, the
   // same values in the same order
@@ -704,8 +804,12 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
   if (cosine) {
     // sample_from_cosine: build_onb_from_w (:133-140) + rand_cos_dir (:123-131)
     const f3 a = (sign_w(w.x) * w.x) > 0.9f ? f3{0.0f, 1.0f, 0.0f} : f3{1.0f, 0.0f, 0.0f};
-    // |w| = 1 +- 2^-22 and a is the axis w is furthest from: |w x a|^2 >= 0.19
-    const f3 v = normalize_unit(cross(w, a));
+    // |w| = 1 +- 2^-22 and a is the axis w is furthest from: |w x a|^2 >= 0.19.  The components
+    // of w x a are 0 or +-w_i (a is a unit axis), so under fast_w 0 or >= 2^-61: a short division
+    const f3 c = cross(w, a);
+    f3 v;
+    if (fast_w) v = div3_by(c, sqrt_fast(dot(c, c)));
+    else v = normalize_unit(c);
     const f3 u = cross(w, v);
     const float z = sqrt_fast(1.0f - r2);
     const float phi = 2.0f * kPI * r1;
@@ -721,34 +825,39 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
   }
   // mixture_pdf (:191-193) = 0.5*cosine_pdf + 0.5*light_area_pdf
   const float len = length(sdir);
-#ifdef WGT_FASTDIV_PROBE
-  const f3 nd = div3_by(sdir, len);
-#else
-  const f3 nd = sdir / len;  // normalize(dir): shared by cosine_pdf, the light cosine and :282
-#endif
+  // normalize(dir) = sdir / len, the light pdf dist2 / (light_cosine * area) and scattering_pdf's
+  // second normalisation nd / |nd| are short divisions when every sdir component is 0 or at least
+  // 2^-90 len and 2^-100 (so nd_i is 0 or >= 2^-91, |nd| = 1 +- 2^-22), and len is in [2^-24, 2^24]
+  // (dist2 in [2^-48, 2^48], the light pdf's denominator in [2^-34, 2^25] for sc.fast_shade's light
+  // area in [2^-24, 2^24]); the test compares float bit patterns: (bits << 1) - 1 maps +-0 to the
+  // largest unsigned value and orders the rest by magnitude.
+  const uint32_t lb = __float_as_uint(len);
+  const int thr = max((int)lb - (90 << 23), (int)__float_as_uint(0x1p-100f));
+  const uint32_t mag = min(min((__float_as_uint(sdir.x) << 1) - 1u, (__float_as_uint(sdir.y) << 1) - 1u),
+                           (__float_as_uint(sdir.z) << 1) - 1u);
+  const bool fast_d = (WGT_SHADE_SHORT & 2) && sc.fast_shade && lb - __float_as_uint(0x1p-24f) <= __float_as_uint(0x1p24f) -
+                      __float_as_uint(0x1p-24f) && mag >= ((uint32_t)thr << 1) - 1u;
+  f3 nd, nd2;
+  float lpdf;
+  if (fast_d) {
+    nd = div3_by(sdir, len);
+    lpdf = div_by(len * len, rcp_of((fabs_w(nd.y) + kRayMin) * sc.light_area));
+    nd2 = div3_by(nd, sqrt_fast(dot(nd, nd)));
+  } else {
+    nd = sdir / len;  // normalize(dir): shared by cosine_pdf, the light cosine and :282
+    const float dist2 = len * len;
+    const float light_cosine = fabs_w(nd.y) + kRayMin;
+    lpdf = dist2 / (light_cosine * sc.light_area);
+    // scattering_pdf (:217-220) normalises the already normalised direction again
+    nd2 = normalize_unit(nd);  // nd = sdir / exact length: unit, NaN or 0
+  }
   const float cs = dot(nd, w);
   const float cpdf = cs <= 0.0f ? 0.0f : cs * k_1_PI;
-  const float dist2 = len * len;
-  const float light_cosine = fabs_w(nd.y) + kRayMin;
-#ifdef WGT_FASTDIV_PROBE
-  const float lpdf = div_by(dist2, rcp_of(light_cosine * sc.light_area));
-#else
-  const float lpdf = dist2 / (light_cosine * sc.light_area);
-#endif
   const float pdf_val = 0.5f * cpdf + 0.5f * lpdf;
-  // scattering_pdf (:217-220) normalises the already normalised direction again
-#ifdef WGT_FASTDIV_PROBE
-  const f3 nd2 = div3_by(nd, sqrt_fast(dot(nd, nd)));
-#else
-  const f3 nd2 = normalize_unit(nd);  // nd = sdir / exact length: unit, NaN or 0
-#endif
   const float cs2 = dot(h.norm, nd2);
   const float spdf = cs2 < 0.0f ? 0.0f : cs2 * k_1_PI;
-#ifdef WGT_FASTDIV_PROBE
-  pc = div3_by(spdf * (pc * h.col), pdf_val);
-#else
+  // the path colour's magnitude is unbounded over bounces: IEEE division
   pc = (spdf * (pc * h.col)) / pdf_val;
-#endif
   ro = h.pos;
   rd = nd;
   return false;
@@ -780,6 +889,7 @@ __device__ __forceinline__ bool px_first(const Pixel& px) { return px.sij == 0u;
 
 struct Counters {
   uint32_t q, tr, nan, lw, ll;
+  uint32_t qref;  // rays whose quad scan took the reference path (quad_scan_fast's almost-ties)
   uint32_t px;  // pixels finished by this lane
 };
 
@@ -874,6 +984,7 @@ __device__ __forceinline__ void flush_counters(unsigned long long* __restrict__ 
   atomicAdd(&counters[CNT_NODES], (unsigned long long)st.nodes);
   atomicAdd(&counters[CNT_TRIS], (unsigned long long)st.tris);
   atomicAdd(&counters[CNT_PIXELS], (unsigned long long)c.px);
+  if (c.qref) atomicAdd(&counters[CNT_QUAD_REF], (unsigned long long)c.qref);
   atomicAdd(&counters[CNT_LOOP_WAVE], (unsigned long long)c.lw);
   atomicAdd(&counters[CNT_LOOP_LANE], (unsigned long long)c.ll);
   atomicAdd(&counters[CNT_TRAV_WAVE], (unsigned long long)st.wave_steps);

@@ -43,11 +43,15 @@ WGT_HD void tri_box(f3 v0, f3 e1, f3 e2, f3& lo, f3& hi) {
 // 1/d with |d| < 1e-30 replaced by copysign(1e-30, d): finite, so slab values are never NaN.
 WGT_HD float safe_inv(float x) {
   if (fabs_w(x) < 1e-30f) x = __builtin_copysignf(1e-30f, x);
-#ifdef WGT_FASTDIV_PROBE
-  return div_by(1.0f, rcp_of(x));
-#else
   return 1.0f / x;
-#endif
+}
+
+// safe_inv by the short reciprocal (wgt_math.h div_by): the IEEE quotient for every 1e-30 <= |x| <=
+// 2^34 (wgt_selftest_math tests each such bit pattern), which holds render rays' directions
+// (primary components within 2^32, scattered ones unit; the clamp gives |x| >= 1e-30)
+WGT_HD float safe_inv_short(float x) {
+  if (fabs_w(x) < 1e-30f) x = __builtin_copysignf(1e-30f, x);
+  return div_by(1.0f, rcp_of(x));
 }
 
 // Slab interval of box [lo, hi] for a ray given as inv = 1/d and ot = -(o * inv):
