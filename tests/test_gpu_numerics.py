@@ -124,6 +124,16 @@ def test_render_limits_fail_cleanly(ctx, wgt):
     cam = wgt.camera_param(1.0, 1, 0)
     cam["origin"][0, 0] = np.nan
     invalid(lambda: ctx.render_tile(cam, 8, 8))
+    # round 6: a pixel's coordinates are the 16-bit halves of one register (frames up to 65,535 on a
+    # side), a pending quad's index + 1 fits 26 bits
+    cam = wgt.camera_param(1.0, 1, 0)
+    invalid(lambda: ctx.render_tile(cam, 65536, 4, 0, 0, 8, 4))
+    from webgputracer_amd._lib import ptr
+
+    # the count is refused before any quad is read: a one-quad buffer with a count of 2^26 - 2
+    invalid(lambda: ctx._check(ctx._L.wgt_upload_scene(ctx.h, ptr(L), len(L), ptr(Q), (1 << 26) - 2, ptr(S),
+                                                       len(S), None, 0)))
+    ctx.upload_scene(L, Q, S)
 
 
 @pytest.mark.parametrize("seed", [1, 2])
@@ -134,17 +144,15 @@ def test_selftest_math_sequences_are_exact(ctx, seed):
     every exponent of the numerator included; denominators up to 2^35, the bound
     2*sqrt(3)*2^32 of |qn . d|), and the IEEE bits of 1/det on 16M determinants over
     Moller-Trumbore's range 2^-40 <= |det| < 2^95 under the limits; since round 6 also the
-    short reciprocal of the traversal's 1/d on every bit pattern 1e-30 <= |x| <= 2^34, and shade's
-    short divisions on 16M operand pairs of each of their three domains (normalisations with
-    |n| / d down to 2^-90 and zeros of either sign, the second normalisation's d = 1 +- k 2^-24, the
-    light pdf), DESIGN.md §3.2."""
+    short reciprocal of the traversal's 1/d on every bit pattern 1e-30 <= |x| <= 2^34 (render rays'
+    direction components after safe_inv's clamp), DESIGN.md §3.2."""
     c = ctx.selftest_math(1 << 24, seed)
     print("selftest", c)
     lo = int(np.float32(1e-30).view(np.uint32))
     hi = int(np.float32(2.0 ** 34).view(np.uint32))
-    # div_tests: 2^24 quad-distance quotients + 2^24 Moller-Trumbore reciprocals 1/det + 3 x 2^24
-    # shading quotients + every traversal reciprocal pattern (both signs)
-    assert c["sqrt_tests"] == 1 << 32 and c["div_tests"] == (5 << 24) + 2 * (hi - lo + 1)
+    # div_tests: 2^24 quad-distance quotients + 2^24 Moller-Trumbore reciprocals 1/det + every
+    # traversal reciprocal pattern (both signs)
+    assert c["sqrt_tests"] == 1 << 32 and c["div_tests"] == (2 << 24) + 2 * (hi - lo + 1)
     assert c["sqrt_fast_tests"] > 3 << 30
     assert c["sqrt_rn_bad"] == 0 and c["sqrt_fast_bad"] == 0 and c["div_rn_bad"] == 0, c
 

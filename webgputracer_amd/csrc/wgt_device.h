@@ -65,12 +65,8 @@ __device__ __forceinline__ void isect_quad(f3 o, f3 d, const float4* __restrict_
   // below, decided before the square root.  qt is +inf until a quad is accepted.
   if (t >= qt) return;
   const f3 pos = o + t * d;
-#ifdef WGT_QUADDIST_PROBE
-  const float ray_dist = t;  // PROBE ONLY: ties of the rounded distance ignored
-#else
   const float ray_dist = distance(pos, o);
   if (ray_dist >= h.dist) return;
-#endif
   const f3 hit_vec = pos - xyz(q[0]);
   const f3 w = xyz(wd);
   const float a = dot(w, cross(hit_vec, xyz(q[2])));
@@ -482,31 +478,6 @@ struct Stack24S {
 };
 using Stack32 = Stack32S<>;
 using Stack24 = Stack24S<>;
-// Stack24 at a fixed layout (k_render_ps at 6 waves per SIMD without parked state): kStackMax + 1
-// entries per lane whatever the tree needs, the 16-bit array at LDS byte 0 and the 8-bit one at
-// kStack24HiOffset, so that entry i of lane l is addressed from one per-lane register, the lane
-// index: ((i << 6) + l) * 2 and ((i << 6) + l) + kStack24HiOffset, the offset an immediate of the
-// LDS instruction.  The pointer-pair form (Stack24) keeps two per-lane addresses live through the
-// whole kernel, which the service code's register pressure spills.
-constexpr uint32_t kStack24Entries = kStackMax + 1;
-constexpr uint32_t kStack24HiOffset = kStack24Entries * kBlock * 2;
-struct Stack24C {
-  uint32_t lane;
-  __device__ __forceinline__ int ld(int i) const {
-    const uint32_t a = ((uint32_t)i << 6) + lane;
-    extern __shared__ int s_stack[];
-    const char* b = (const char*)s_stack;
-    return ((int)*(const int8_t*)(b + kStack24HiOffset + a) << 16) | (int)*(const uint16_t*)(b + 2 * a);
-  }
-  __device__ __forceinline__ void st(int i, int v) const {
-    const uint32_t a = ((uint32_t)i << 6) + lane;
-    extern __shared__ int s_stack[];
-    char* b = (char*)s_stack;
-    *(uint16_t*)(b + 2 * a) = (uint16_t)v;
-    *(int8_t*)(b + kStack24HiOffset + a) = (int8_t)(v >> 16);
-  }
-};
-
 // Parked traversal state of k_render_ps (DevScene::ps_park): the
 // lane's Trav lives in LDS words (stride kBlock, conflict-free) while its wave runs a
 // service pass, so the service code does not hold the traversing lanes' 11 registers and
@@ -769,11 +740,6 @@ struct Light {
   f3 pos, right, up;
 };
 
-// shade's short divisions (A/B builds): bit 0 the normal's normalisations, bit 1 the sampled
-// direction's (and the light pdf)
-#ifndef WGT_SHADE_SHORT
-#define WGT_SHADE_SHORT 0
-#endif
 // raytrace() after sample_hit (path_tracer.wgsl:267-287).  Returns path.end.
 __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const Hit& h, int depth,
                                       uint32_t& seed, f3& ro, f3& rd, f3& pc) {
@@ -786,15 +752,9 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
     }
     return true;
   }
-  // sample_direction (path_tracer.wgsl:146-154); onb.w of build_onb_from_w(hit.norm).  Short
-  // divisions (div3_by) where they are the IEEE quotient ("shading divisions"):
-  // the scene's quad and triangle normals are unit within 2^-10 with no component below 2^-60 in
-  // magnitude but 0 (sc.fast_shade, checked at upload), so |n_i| / |n| is 0 or >= 2^-61 with |n|
-  // in [1/2, 2]; a sphere's normal is computed per hit and takes the IEEE division.
-  const bool fast_w = (WGT_SHADE_SHORT & 1) && sc.fast_shade && h.prim < sc.first_sphere;
-  f3 w;
-  if (fast_w) w = div3_by(h.norm, length(h.norm));
-  else w = normalize(h.norm);
+  // sample_direction (path_tracer.wgsl:146-154).  The shading divisions stay IEEE: short forms
+  // behind wave-uniform range tests measured slower
+  const f3 w = normalize(h.norm);  // onb.w of build_onb_from_w(hit.norm)
   f3 sdir;
   // both branches draw two more rand() (r1 then r2) right away: drawn once here, the
   // same values in the same order
@@ -804,12 +764,8 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
   if (cosine) {
     // sample_from_cosine: build_onb_from_w (:133-140) + rand_cos_dir (:123-131)
     const f3 a = (sign_w(w.x) * w.x) > 0.9f ? f3{0.0f, 1.0f, 0.0f} : f3{1.0f, 0.0f, 0.0f};
-    // |w| = 1 +- 2^-22 and a is the axis w is furthest from: |w x a|^2 >= 0.19.  The components
-    // of w x a are 0 or +-w_i (a is a unit axis), so under fast_w 0 or >= 2^-61: a short division
-    const f3 c = cross(w, a);
-    f3 v;
-    if (fast_w) v = div3_by(c, sqrt_fast(dot(c, c)));
-    else v = normalize_unit(c);
+    // |w| = 1 +- 2^-22 and a is the axis w is furthest from: |w x a|^2 >= 0.19
+    const f3 v = normalize_unit(cross(w, a));
     const f3 u = cross(w, v);
     const float z = sqrt_fast(1.0f - r2);
     const float phi = 2.0f * kPI * r1;
@@ -825,38 +781,17 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
   }
   // mixture_pdf (:191-193) = 0.5*cosine_pdf + 0.5*light_area_pdf
   const float len = length(sdir);
-  // normalize(dir) = sdir / len, the light pdf dist2 / (light_cosine * area) and scattering_pdf's
-  // second normalisation nd / |nd| are short divisions when every sdir component is 0 or at least
-  // 2^-90 len and 2^-100 (so nd_i is 0 or >= 2^-91, |nd| = 1 +- 2^-22), and len is in [2^-24, 2^24]
-  // (dist2 in [2^-48, 2^48], the light pdf's denominator in [2^-34, 2^25] for sc.fast_shade's light
-  // area in [2^-24, 2^24]); the test compares float bit patterns: (bits << 1) - 1 maps +-0 to the
-  // largest unsigned value and orders the rest by magnitude.
-  const uint32_t lb = __float_as_uint(len);
-  const int thr = max((int)lb - (90 << 23), (int)__float_as_uint(0x1p-100f));
-  const uint32_t mag = min(min((__float_as_uint(sdir.x) << 1) - 1u, (__float_as_uint(sdir.y) << 1) - 1u),
-                           (__float_as_uint(sdir.z) << 1) - 1u);
-  const bool fast_d = (WGT_SHADE_SHORT & 2) && sc.fast_shade && lb - __float_as_uint(0x1p-24f) <= __float_as_uint(0x1p24f) -
-                      __float_as_uint(0x1p-24f) && mag >= ((uint32_t)thr << 1) - 1u;
-  f3 nd, nd2;
-  float lpdf;
-  if (fast_d) {
-    nd = div3_by(sdir, len);
-    lpdf = div_by(len * len, rcp_of((fabs_w(nd.y) + kRayMin) * sc.light_area));
-    nd2 = div3_by(nd, sqrt_fast(dot(nd, nd)));
-  } else {
-    nd = sdir / len;  // normalize(dir): shared by cosine_pdf, the light cosine and :282
-    const float dist2 = len * len;
-    const float light_cosine = fabs_w(nd.y) + kRayMin;
-    lpdf = dist2 / (light_cosine * sc.light_area);
-    // scattering_pdf (:217-220) normalises the already normalised direction again
-    nd2 = normalize_unit(nd);  // nd = sdir / exact length: unit, NaN or 0
-  }
+  const f3 nd = sdir / len;  // normalize(dir): shared by cosine_pdf, the light cosine and :282
   const float cs = dot(nd, w);
   const float cpdf = cs <= 0.0f ? 0.0f : cs * k_1_PI;
+  const float dist2 = len * len;
+  const float light_cosine = fabs_w(nd.y) + kRayMin;
+  const float lpdf = dist2 / (light_cosine * sc.light_area);
   const float pdf_val = 0.5f * cpdf + 0.5f * lpdf;
+  // scattering_pdf (:217-220) normalises the already normalised direction again
+  const f3 nd2 = normalize_unit(nd);  // nd = sdir / exact length: unit, NaN or 0
   const float cs2 = dot(h.norm, nd2);
   const float spdf = cs2 < 0.0f ? 0.0f : cs2 * k_1_PI;
-  // the path colour's magnitude is unbounded over bounces: IEEE division
   pc = (spdf * (pc * h.col)) / pdf_val;
   ro = h.pos;
   rd = nd;
@@ -871,7 +806,7 @@ __device__ __forceinline__ uint8_t unorm8(float x) {
 
 // Per-pixel state shared by both kernels.
 struct Pixel {
-  uint32_t x, y;
+  uint32_t xy;  // x | y << 16 (frames are at most 65535 x 65535, check_render_args): one register
   uint32_t seed;
   uint32_t sij;  // the sample's s_i | s_j << 16 (sqrt_spp < 2^16); index = s_i + s_j * sqrt_spp
   f3 col;
@@ -893,6 +828,16 @@ struct Counters {
   uint32_t px;  // pixels finished by this lane
 };
 
+// x / d for d >= 1 with m = (2^32 - 1) / d (host): mulhi(x, m) is x / d or up to two less
+// (x m / 2^32 > x / d - x / 2^32 - x / (d 2^32) - 1 > x / d - 3 for x < 2^32), fixed by two steps.
+__device__ __forceinline__ uint32_t udiv_by(uint32_t x, uint32_t d, uint32_t m) {
+  uint32_t q = __umulhi(x, m);
+  uint32_t r = x - q * d;
+  if (r >= d) { ++q; r -= d; }
+  if (r >= d) ++q;
+  return q;
+}
+
 // Pixel of pixel slot (block, lane) = (slot >> 6, slot & 63): block b covers an
 // 8x8 sub-block of tile b / (sub-blocks per tile).  false if the slot is outside
 // its tile or the frame.  po = the pixel's offset in the tile-major output
@@ -901,16 +846,19 @@ __device__ __forceinline__ bool slot_setup(const DevFrame& fr, const wgt_tile* _
                                            uint32_t block, uint32_t lane, uint32_t& po, Pixel& px) {
   const uint32_t bx = (fr.tw + 7u) >> 3, by = (fr.th + 7u) >> 3;
   const uint32_t bpt = bx * by;
-  const uint32_t tile = block / bpt;
+  // divisions by the host's multipliers (DevFrame::div_bx, div_bpt): no per-lane reciprocal kept
+  // live through the kernel, where the compiler's division by a runtime value would hoist one
+  const uint32_t tile = udiv_by(block, bpt, fr.div_bpt);
   const uint32_t rem = block - tile * bpt;
-  const uint32_t lx = (rem % bx) * 8u + (lane & 7u);
-  const uint32_t ly = (rem / bx) * 8u + (lane >> 3);
+  const uint32_t ry = udiv_by(rem, bx, fr.div_bx);
+  const uint32_t lx = (rem - ry * bx) * 8u + (lane & 7u);
+  const uint32_t ly = ry * 8u + (lane >> 3);
   if (tile >= fr.n_tiles || lx >= fr.tw || ly >= fr.th) return false;
   const wgt_tile td = tiles[tile];
-  px.x = td.x0 + lx;
-  px.y = td.y0 + ly;
-  if (px.x >= fr.W || px.y >= fr.H) return false;  // path_tracer.wgsl:377
-  px.seed = px.x + px.y * fr.W + td.seed * fr.W * fr.H;  // path_tracer.wgsl:378
+  const uint32_t x = td.x0 + lx, y = td.y0 + ly;
+  if (x >= fr.W || y >= fr.H) return false;  // path_tracer.wgsl:377
+  px.xy = x | y << 16;
+  px.seed = x + y * fr.W + td.seed * fr.W * fr.H;  // path_tracer.wgsl:378
   px.sij = 0u;
   px.col = f3{0.0f, 0.0f, 0.0f};
   po = (tile * fr.th + ly) * fr.tw + lx;
@@ -928,7 +876,7 @@ __device__ __forceinline__ void camera_ray(const DevFrame& fr, Pixel& px, f3& ro
   const f3 origin = f3{fr.ox, fr.oy, fr.oz};
   const f3 du = f3{fr.dux, fr.duy, fr.duz};
   const f3 dv = f3{fr.dvx, fr.dvy, fr.dvz};
-  const f3 pixel_center = (f3{fr.pox, fr.poy, fr.poz} + (float)px.x * du) + (float)px.y * dv;
+  const f3 pixel_center = (f3{fr.pox, fr.poy, fr.poz} + (float)(px.xy & 0xffffu) * du) + (float)(px.xy >> 16) * dv;
   const float sx = -0.5f + fr.recip_sqrt_spp * ((float)px_si(px) + rand_next(px.seed));
   const float sy = -0.5f + fr.recip_sqrt_spp * ((float)px_sj(px) + rand_next(px.seed));
   const f3 pixel_sample = pixel_center + (sx * du + sy * dv);

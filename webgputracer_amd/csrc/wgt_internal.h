@@ -54,10 +54,6 @@ struct DevScene {
   uint32_t n_nodes;
   uint32_t last_sphere_emissive;
   float light_area;  // length(cross(lights[0].right, lights[0].up)) (path_tracer.wgsl:205)
-  // shade's short divisions (wgt_device.h): 1 when every quad normal and triangle face normal is
-  // NaN or unit within 2^-10 with each component 0 or >= 2^-60 in magnitude, and the light area is
-  // in [2^-24, 2^24] (wgt_runtime.cpp fast_shade_ok); first_sphere = the first sphere's prim id
-  uint32_t fast_shade, first_sphere;
   uint32_t stack;     // traversal stack entries per lane (>= 1)
   // k_render_ps waves per SIMD: 6 (3-byte stack entries, Stack24) when every ref of
   // the tree fits 24 bits (kStack24Nodes, kStack24Tris), else 5
@@ -82,11 +78,9 @@ constexpr uint32_t kMinPsCap = 8;
 inline size_t stack_lds_bytes(const DevScene& sc) { return (size_t)sc.stack * kBlock * sizeof(int); }
 // ... of a k_render_ps launch: 3-byte entries at 6 waves per SIMD, ps_cap entries and
 // the parked state when ps_park
-// (6 waves without parked state: the fixed layout of kStackMax + 1 entries, wgt_device.h Stack24C)
 inline size_t ps_stack_lds_bytes(const DevScene& sc) {
   const size_t entry = sc.ps_waves >= 6 ? 3 : sizeof(int);
   if (sc.ps_park) return (size_t)sc.ps_cap * kBlock * entry + (size_t)kParkWords * kBlock * 4;
-  if (sc.ps_waves == 6 && sc.n_tris > 0) return (size_t)(kStackMax + 1) * kBlock * 3;
   return (size_t)sc.stack * kBlock * entry;
 }
 // LDS entries the parked kernel can hold at its wave budget: the stack and the parked words
@@ -147,6 +141,9 @@ struct DevFrame {
   // of the lane (wave w, lane l) at ps_spill[e * ps_spill_stride + w * 64 + l] (launch_render)
   int* ps_spill;
   uint32_t ps_spill_stride;
+  // (2^32 - 1) / d for the 8x8 blocks per tile row (bx) and per tile (bx * by) of the launch
+  // (launch_render): slot_setup's divisions by them (wgt_device.h udiv_by)
+  uint32_t div_bx, div_bpt;
 };
 
 enum {

@@ -111,15 +111,6 @@ k_render(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* _
 // LDS words (Park) while the wave runs a service pass, and the LDS holds sc.ps_cap stack
 // entries per lane with the rest on a per-lane global stack (park_fix): the service code
 // then holds no traversal registers, which it used to spill to scratch.
-#ifndef WGT_CONST_STACK
-#define WGT_CONST_STACK 0
-#endif
-#ifndef WGT_OT_REMAT
-#define WGT_OT_REMAT 1
-#endif
-#ifndef WGT_INV_REMAT
-#define WGT_INV_REMAT 1
-#endif
 template <bool STATS, bool COST, int CN, int W, bool TRIS = true, bool PK = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W)))
 k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4* __restrict__ out8,
@@ -130,10 +121,8 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   // noalias pointer, so its stores do not clobber the scene for the compiler, whose
   // wave-uniform loads (quads, spheres, the root node) stay scalar loads
   extern __shared__ int s_stack[];  // stack entries per lane (+ parked words), ps_stack_lds_bytes
-  // 6 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit), at the fixed
-  // layout (Stack24C) unless the parked state shares the LDS
-  using STK = typename std::conditional<W >= 6, typename std::conditional<PK || !WGT_CONST_STACK, Stack24, Stack24C>::type,
-                                        Stack32>::type;
+  // 6 waves per SIMD: 3-byte entries (DevScene::ps_waves guarantees the refs fit)
+  using STK = typename std::conditional<W >= 6, Stack24, Stack32>::type;
   const uint32_t cap = PK ? sc.ps_cap : sc.stack;  // LDS stack entries per lane
   // PK: the highest stack top a node step may start from, cap - 4 (3 pushes and a parked
   // leaf above it); no bound when the LDS holds the builder's whole stack (cap = sc.stack),
@@ -141,10 +130,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   const uint32_t top_max = PK && cap < sc.stack ? cap - 4u : 0xffffffffu;
   STK lds;
   Park P;
-  if constexpr (std::is_same<STK, Stack24C>::value) {
-    lds.lane = threadIdx.x;
-    P.p = nullptr;  // no parked state (PK = false)
-  } else if constexpr (W >= 6) {
+  if constexpr (W >= 6) {
     lds.lo = (uint16_t*)s_stack + threadIdx.x;
     lds.hi = (int8_t*)((uint16_t*)s_stack + cap * kBlock) + threadIdx.x;
     P.p = (uint32_t*)((char*)s_stack + cap * kBlock * 3) + threadIdx.x;
@@ -159,7 +145,9 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
   Pixel px{};
   uint32_t po = 0;  // output offset of the lane's pixel
   f3 ro{}, rd{}, pc{};
-  int depth = 0;
+  // the path depth and the pending hit's quad (quad_scan_fast; kNoHit + 1 = 0 for none), one
+  // register: depth | (q_prim + 1) << 6 (depth <= kRayDepth < 64, quads < 2^26 at upload)
+  uint32_t dq = 0;
   TravStats st{};
   Counters c{0u, 0u, 0u, 0u, 0u, 0u, 0u};
   // invariant: trav == !trav_done(t) (a lane leaves the traversal exactly when
@@ -177,7 +165,6 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
     park_put(P, t);
     P.st(9, 0u);
   }
-  uint32_t q_prim = kNoHit;  // quad part of the pending hit, rebuilt at finalisation
   float q_t = kRayMax;
   bool have = false;       // lane holds a pixel
   bool exhausted = false;  // the queue is empty for this lane
@@ -227,7 +214,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
               const uint32_t b = fr.perm ? fr.perm[sb] : sb;
               if (slot_setup(fr, tiles, b, sl, po, px)) {
                 have = true;
-                depth = 0;
+                dq = 0u;
                 pblock = b;
               }
             }
@@ -272,17 +259,17 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             const uint32_t bi = PK ? P.ld(7) : t.bi;
             // no triangles (TRIS = false): no shading record exists to preload
             WGT_REGION(cr_fin, float4 pre[2]; if (TRIS) preload_tshade(sc, bi, pre[0], pre[1]);
-                       quad_rebuild(sc, ro, rd, q_prim, q_t, h); finish_hit(sc, ro, rd, bt, bi, h, TRIS ? pre : nullptr));
+                       quad_rebuild(sc, ro, rd, (dq >> 6) - 1u, q_t, h); finish_hit(sc, ro, rd, bt, bi, h, TRIS ? pre : nullptr));
             if (STATS) { ++c.q; ++c.tr; }
           }
-          first_hit(px, depth, h.prim, po, outhit);
+          first_hit(px, (int)(dq & 63u), h.prim, po, outhit);
           const uint64_t ts0 = STATS ? __builtin_amdgcn_s_memtime() : 0;
-          const bool end = shade(sc, L, h, depth, px.seed, ro, rd, pc);
-          ++depth;
+          const bool end = shade(sc, L, h, (int)(dq & 63u), px.seed, ro, rd, pc);
+          dq = (dq & 63u) + 1u;  // the quad is used: q_prim + 1 = 0
           // COST: the pre-pass's paths may end early (DevFrame::pq_depth): a cost estimate
-          if (end || depth == (COST ? (int)fr.pq_depth : kRayDepth)) {
+          if (end || dq == (COST ? fr.pq_depth : (uint32_t)kRayDepth)) {
             end_sample(fr, px, pc);
-            depth = 0;
+            dq = 0u;
           }
           if (STATS) cr_shade += __builtin_amdgcn_s_memtime() - ts0;
           pending = false;
@@ -294,15 +281,15 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             fin = true;
             break;
           }
-          if (depth == 0) {
+          if ((dq & 63u) == 0u) {
             WGT_REGION(cr_cam, camera_ray(fr, px, ro, rd));
             pc = f3{1.0f, 1.0f, 1.0f};
           }
           if (has_nan(ro) || has_nan(rd)) {
             if (!sc.last_sphere_emissive) {
-              first_hit(px, depth, last_prim(sc), po, outhit);
-              skip_nan_path<STATS>(sc, fr, px, depth, c);
-              depth = 0;
+              first_hit(px, (int)(dq & 63u), last_prim(sc), po, outhit);
+              skip_nan_path<STATS>(sc, fr, px, (int)(dq & 63u), c);
+              dq = 0u;
               continue;
             }
             // emissive last sphere: the NaN ray's hit (the last sphere, no traversal)
@@ -311,8 +298,10 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
             pending = true;
             break;
           }
+          uint32_t q_prim;
           WGT_REGION(cr_quads, const bool qx = quad_scan_fast(sc, ro, rd, q_prim, q_t);
                      if (STATS && !qx) ++c.qref; trav_init<CN>(sc, ro, rd, q_prim != kNoHit, q_t, t));
+          dq = (dq & 63u) | (q_prim + 1u) << 6;
           if (COST) work += fr.pq_svc_cost;
           // the root node is tested here: rays that miss every root child never
           // enter the traversal phase
@@ -351,22 +340,14 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
     // finished one (a lane parked on its LDS bound is served before the next traversal
     // phase: the first iteration of a service phase serves every lane that needs it)
     if (PK && TRIS) park_get(P, t);
-#if WGT_OT_REMAT
-    // the slab offsets -o / d are recomputed here from the ray and 1/d (the same operations as
-    // trav_init: bit-identical), so that they are dead through the service phase: three fewer
-    // registers where its pressure spills.  Under CN t.inv holds s/d, and
-    // (s/d) * (1/s) = 1/d exactly
-#if WGT_INV_REMAT
-    // and 1/d too (trav_init's operations: bit-identical)
+    // 1/d and the slab offsets -o / d are recomputed here from the ray (trav_init's operations:
+    // bit-identical), so that they are dead through the service phase: six fewer registers where
+    // its pressure spilled (scratch 52 -> 20 B/lane, sponza +4.4 %)
     if (!PK && TRIS) {
       const f3 inv = f3{safe_inv_short(rd.x), safe_inv_short(rd.y), safe_inv_short(rd.z)};
       t.ot = slab_offset(ro, inv);
       t.inv = CN ? sc.cstep * inv : inv;
     }
-#else
-    if (!PK && TRIS) t.ot = slab_offset(ro, CN ? sc.rcstep * t.inv : t.inv);
-#endif
-#endif
     bool parked = false;  // PK: the lane left on its LDS stack bound, its state parked as it was
     for (; TRIS;) {
       // one uniform mode per step: triangle steps once enough lanes hold a
@@ -506,10 +487,6 @@ k_lpt_order(uint32_t* __restrict__ cost, uint32_t blocks, uint32_t* __restrict__
 //             |det| < 2^95 (the render limits' range past the 1e-12 rejection): its bits;
 //   the short reciprocal of the traversal's 1/d (trav_init, render rays: safe_inv_short) on every
 //             bit pattern with 1e-30 <= |x| <= 2^34;
-//   shade's short divisions div_by (wgt_device.h shade) on n pairs of each of their domains:
-//             normalisations, n in {+-0} u [max(2^-90 d, 2^-100), 2 d] with 2^-40 <= d < 2^44; the
-//             second normalisation, d = 1 +- k 2^-24 (k <= 8) with n in {+-0} u [2^-91, 1.0001];
-//             the light pdf, 2^-48 <= |n| < 2^48 over 2^-34 <= d < 2^25;
 //   the compiler's own lowerings (__builtin_sqrtf, n / d) on the same inputs.
 // NaN equals NaN.  counts: [0] sqrt tests, [1] sqrt_rn bad, [2] div tests, [3]
 // div_rn bad, [4] sqrt_fast tests, [5] sqrt_fast bad, [6] compiler sqrt bad, [7]
@@ -529,7 +506,7 @@ __device__ __forceinline__ bool st_same(float a, float b) {
 __device__ __forceinline__ bool st_accept(float t) { return !(t < kRayMin || kRayMax < t); }
 __global__ void __launch_bounds__(256) k_selftest_math(uint32_t n, uint32_t seed, unsigned long long* counts) {
   uint32_t bad_s = 0, bad_f = 0, n_f = 0, bad_d = 0, bad_sc = 0, bad_dc = 0;
-  uint32_t dbg[4] = {0u, 0u, 0u, 0u};  // the failures of the short forms' domains, apart (WGT_SELFTEST_DEBUG)
+  uint32_t bad_r = 0;  // the traversal reciprocal's failures
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t i = blockIdx.x * blockDim.x + threadIdx.x; i < (1ull << 32); i += stride) {
     const uint32_t bits = (uint32_t)i;
@@ -544,7 +521,7 @@ __global__ void __launch_bounds__(256) k_selftest_math(uint32_t n, uint32_t seed
       bad_f += st_same(sqrt_fast(x), ref) ? 0u : 1u;
     }
     if (mag >= __float_as_uint(1e-30f) && mag <= __float_as_uint(0x1p34f))
-      dbg[0] += st_same(safe_inv_short(x), (float)(1.0 / (double)x)) ? 0u : 1u;
+      bad_r += st_same(safe_inv_short(x), (float)(1.0 / (double)x)) ? 0u : 1u;
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint32_t)stride) {
     const uint32_t h = st_hash(seed * 0x9e3779b9u + i), h2 = st_hash(h ^ 0x5bd1e995u);
@@ -561,33 +538,8 @@ __global__ void __launch_bounds__(256) k_selftest_math(uint32_t n, uint32_t seed
     const float rref = (float)(1.0 / (double)det);
     bad_d += st_same(div_rn(1.0f, det), rref) ? 0u : 1u;
     bad_dc += st_same(1.0f / det, rref) ? 0u : 1u;
-    // shade's normalisations: |n| / d in [2^-90, 2], |n| >= 2^-100, or n = +-0 (1 in 16)
-    const uint32_t h3 = st_hash(h2 ^ 0x68e31da4u), h4 = st_hash(h3 ^ 0x1b873593u);
-    const float dn = st_float(h3, 127u - 40u, 127u + 43u);
-    const uint32_t ed = (__float_as_uint(dn) >> 23) & 0xffu;
-    int en = (int)ed - 90 + (int)((h4 >> 8) % 92u);  // the exponent of n in [e(d) - 90, e(d) + 1]
-    en = en < 27 ? 27 : en;                            // >= 2^-100
-    float nn2 = __uint_as_float((h4 & 0x80000000u) | ((uint32_t)en << 23) | (st_hash(h4) & 0x7fffffu));
-    if ((h4 & 15u) == 0u) nn2 = (h4 & 0x80000000u) ? -0.0f : 0.0f;
-    dbg[1] += st_same(div_by(nn2, rcp_of(dn)), (float)((double)nn2 / (double)dn)) ? 0u : 1u;
-    // the second normalisation: d = 1 +- k 2^-24, n in {+-0} u [2^-91, 1.0001]
-    const float d1 = __uint_as_float(__float_as_uint(1.0f) + (h3 & 8u ? 0u - (h3 & 7u) : (h3 & 7u)));
-    float n1 = st_float(h4 ^ 0x2545f491u, 127u - 91u, 127u);
-    if ((h3 & 48u) == 0u) n1 = (h3 & 64u) ? -0.0f : 0.0f;
-    dbg[2] += st_same(div_by(n1, rcp_of(d1)), (float)((double)n1 / (double)d1)) ? 0u : 1u;
-    // the light pdf dist2 / (light_cosine * area)
-    const float nl = st_float(st_hash(h4 ^ 0x85ebca6bu), 127u - 48u, 127u + 47u);
-    const float dl = fabsf(st_float(st_hash(h3 ^ 0xc2b2ae35u), 127u - 34u, 127u + 24u));
-    dbg[3] += st_same(div_by(nl, rcp_of(dl)), (float)((double)nl / (double)dl)) ? 0u : 1u;
   }
-#ifdef WGT_SELFTEST_DEBUG  // a diagnostic build: the four short-form domains' failures in counts[4..7]
-  atomicAdd(&counts[4], (unsigned long long)dbg[0]);
-  atomicAdd(&counts[5], (unsigned long long)dbg[1]);
-  atomicAdd(&counts[6], (unsigned long long)dbg[2]);
-  atomicAdd(&counts[7], (unsigned long long)dbg[3]);
-  return;
-#endif
-  bad_d += dbg[0] + dbg[1] + dbg[2] + dbg[3];
+  bad_d += bad_r;
   atomicAdd(&counts[1], (unsigned long long)bad_s);
   atomicAdd(&counts[3], (unsigned long long)bad_d);
   atomicAdd(&counts[4], (unsigned long long)n_f);
@@ -661,6 +613,9 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   const uint64_t blocks = (uint64_t)bx * by * fr.n_tiles;
   if (blocks == 0) return hipSuccess;
   if (blocks > 0x7fffffffull) return hipErrorInvalidValue;
+  DevFrame fm = fr;  // + slot_setup's division multipliers
+  fm.div_bx = 0xffffffffu / bx;
+  fm.div_bpt = 0xffffffffu / (bx * by);
   const dim3 block(kBlock);
   const size_t lds = stack_lds_bytes(sc);
   const bool tris = sc.n_tris > 0;
@@ -675,7 +630,7 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
     const bool lpt = fr.pq_lpt && fr.sqrt_spp > fr.pq_lpt;
     const int cn = node_form(sc, fr);
     uint32_t* q = (uint32_t*)ws;
-    DevFrame f = fr;
+    DevFrame f = fm;
     // phase thresholds swept per wave budget (profiles/sweeps/r01_sweep_compact_knobs.jsonl)
     if (f.ps_to_trav == 0) f.ps_to_trav = sc.ps_waves >= 6 ? 16u : 18u;
     if (f.ps_to_service == 0) f.ps_to_service = sc.ps_waves >= 6 ? 14u : 16u;
@@ -715,11 +670,11 @@ hipError_t launch_render(const DevScene& sc, const DevFrame& fr, const wgt_tile*
   }
   const dim3 grid((uint32_t)blocks);
   if (counters) {
-    if (tris) k_render<true, true><<<grid, block, lds, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
-    else k_render<false, true><<<grid, block, lds, stream>>>(sc, fr, d_tiles, out8, out32, outhit, counters);
+    if (tris) k_render<true, true><<<grid, block, lds, stream>>>(sc, fm, d_tiles, out8, out32, outhit, counters);
+    else k_render<false, true><<<grid, block, lds, stream>>>(sc, fm, d_tiles, out8, out32, outhit, counters);
   } else {
-    if (tris) k_render<true, false><<<grid, block, lds, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
-    else k_render<false, false><<<grid, block, lds, stream>>>(sc, fr, d_tiles, out8, out32, outhit, nullptr);
+    if (tris) k_render<true, false><<<grid, block, lds, stream>>>(sc, fm, d_tiles, out8, out32, outhit, nullptr);
+    else k_render<false, false><<<grid, block, lds, stream>>>(sc, fm, d_tiles, out8, out32, outhit, nullptr);
   }
   return hipGetLastError();
 }

@@ -106,11 +106,12 @@ WGT_HD float div_rn(float n, float d) {
   return n / d;
 #endif
 }
-// Division by a shared denominator: the reciprocal refined once (rcp_of), then per
-// numerator div_rn's two residual corrections and v_div_fixup (div_by), which sets the
-// sign, zeros, infinities and NaNs as the IEEE sequence does.  Without v_div_scale the
-// result is the IEEE quotient when the operands are in the unscaled domain (wgt_math.h
-// div_safe); callers take it only under that guard.
+// Division as the compiler's IEEE sequence without v_div_scale: the reciprocal refined once
+// (rcp_of), then div_rn's two residual corrections and v_div_fixup (div_by), which sets the
+// sign, zeros, infinities and NaNs as the IEEE sequence does.  The result is the IEEE quotient
+// when v_div_scale would not scale (normal operands and quotient well inside the exponent
+// range); its one use, the traversal's 1/d (wgt_geom.h safe_inv_short), is checked on every
+// input it can take (wgt_selftest_math).
 struct RcpF {
   float d, r;
 };
@@ -132,10 +133,6 @@ WGT_HD float div_by(float n, RcpF R) {
 #else
   return n / R.d;
 #endif
-}
-WGT_HD f3 div3_by(f3 a, float s) {
-  const RcpF R = rcp_of(s);
-  return f3{div_by(a.x, R), div_by(a.y, R), div_by(a.z, R)};
 }
 WGT_HD float length(f3 a) { return sqrt_rn(dot(a, a)); }
 // WGSL normalize(v) = v / length(v)   (zero vector -> NaN, as the reference relies on)

@@ -265,27 +265,6 @@ std::string check_scene_limits(const wgt_quad* lq, uint32_t nlq, const wgt_spher
 
 double sq(double x) { return x * x; }
 
-// A normal whose shading divisions are short ones (wgt_device.h shade): NaN (a degenerate
-// primitive: the divisions give NaN either way), or unit within 2^-10 with every component 0 or
-// at least 2^-60 in magnitude.
-bool shade_normal_ok(const float* n) {
-  if (n[0] != n[0] || n[1] != n[1] || n[2] != n[2]) return true;
-  for (int c = 0; c < 3; ++c)
-    if (n[c] != 0.0f && !(std::fabs((double)n[c]) >= 0x1p-60)) return false;
-  return std::fabs(sq(n[0]) + sq(n[1]) + sq(n[2]) - 1.0) <= 0x1p-10;
-}
-uint32_t fast_shade_ok(const wgt_quad* lights, uint32_t nl, const wgt_quad* quads, uint32_t nq,
-                       const wgt_triangle* tris, uint32_t nt, float light_area) {
-  if (!(light_area >= 0x1p-24f && light_area <= 0x1p24f)) return 0u;
-  for (uint32_t i = 0; i < nl; ++i)
-    if (!shade_normal_ok(lights[i].norm)) return 0u;
-  for (uint32_t i = 0; i < nq; ++i)
-    if (!shade_normal_ok(quads[i].norm)) return 0u;
-  for (uint32_t i = 0; i < nt; ++i)
-    if (!shade_normal_ok(tris[i].face_norm)) return 0u;
-  return 1u;
-}
-
 // Largest |coordinate| any point of the scene's primitives can have (quad corners,
 // sphere boxes, triangle vertices): hit points, i.e. secondary ray origins, lie
 // within it.  The compact nodes are built for ray origins within 4x this bound,
@@ -320,6 +299,8 @@ int check_render_args(wgt_ctx* ctx, const wgt_camera_param* cam, uint32_t W, uin
     return fail(ctx, WGT_E_INVALID, "NaN camera parameter");
   // the kernels pack a sample's (s_i, s_j) into 16 bits each and count sqrt_spp^2
   // samples in 32 bits: u32(sqrt(f32(spp))) must stay <= 65535 (spp < 2^32 - 2^8)
+  // the kernels keep a pixel's coordinates as 16-bit halves of one register (wgt_device.h Pixel)
+  if (W > 65535u || H > 65535u) return fail(ctx, WGT_E_INVALID, "frame width and height must be <= 65535");
   if ((uint32_t)__builtin_sqrtf((float)cam->spp) > 65535u)
     return fail(ctx, WGT_E_INVALID, "spp too large (u32(sqrt(f32(spp))) must be <= 65535)");
   if (!finite_within(cam->origin, 3, kCoordLimit) || !finite_within(cam->target, 3, kCoordLimit))
@@ -591,6 +572,8 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
     return fail(ctx, WGT_E_INVALID, "need >= 1 sphere (the reference binds a dummy sphere)");
   if (n_quads > 0 && !quads) return fail(ctx, WGT_E_INVALID, "null quads");
   if (n_tris > 0 && !tris) return fail(ctx, WGT_E_INVALID, "null triangles");
+  // the persistent kernel keeps a pending quad hit's index + 1 in 26 bits (wgt_kernels.hip dq)
+  if ((uint64_t)n_lights + n_quads >= (1u << 26) - 1u) return fail(ctx, WGT_E_INVALID, "too many lights and quads");
   {
     std::string lim = check_scene_limits(lights, n_lights, spheres, n_spheres, tris, n_tris);
     if (lim.empty() && n_quads) lim = check_scene_limits(quads, n_quads, nullptr, 0, nullptr, 0);
@@ -708,9 +691,6 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
   const f3 lr = f3{lights[0].right[0], lights[0].right[1], lights[0].right[2]};
   const f3 lu = f3{lights[0].up[0], lights[0].up[1], lights[0].up[2]};
   sc.light_area = length(cross(lr, lu));  // path_tracer.wgsl:205
-  sc.fast_shade = env_u32("WGT_IEEE_SHADE", 0) ? 0u
-                                                : fast_shade_ok(lights, n_lights, quads, n_quads, tris, n_tris, sc.light_area);
-  sc.first_sphere = n_lights + n_quads + n_tris;
   // + 1: the speculative traversal parks a second leaf on the stack (wgt_device.h)
   sc.stack = (bvh.stack_need > 0 ? bvh.stack_need : 1u) + 1u;
   sc.ps_waves = waves;
@@ -936,13 +916,13 @@ int wgt_selftest_math(wgt_ctx* ctx, uint32_t n, uint32_t seed, uint64_t counts[8
   WGT_HIP(ctx, hipMemcpyAsync(counts, ctx->prim.p, 64, hipMemcpyDeviceToHost, ctx->stream));
   WGT_HIP(ctx, hipStreamSynchronize(ctx->stream));
   counts[0] = 1ull << 32;  // sqrt: every bit pattern
-  // n quad-distance quotients, n Moller-Trumbore reciprocals, 3 n shading quotients, and every
-  // pattern 1e-30 <= |x| <= 2^34 of the traversal's reciprocal
+  // n quad-distance quotients, n Moller-Trumbore reciprocals, and every pattern 1e-30 <= |x| <= 2^34
+  // of the traversal's reciprocal
   uint32_t lo, hi;
   const float flo = 1e-30f, fhi = 0x1p34f;
   std::memcpy(&lo, &flo, 4);
   std::memcpy(&hi, &fhi, 4);
-  counts[2] = 5ull * n + 2ull * (hi - lo + 1u);
+  counts[2] = 2ull * n + 2ull * (hi - lo + 1u);
   return WGT_OK;
 }
 
