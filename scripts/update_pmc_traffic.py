@@ -1,4 +1,4 @@
-"""Write the live PMC figures of a gpurun_out/<tag> run of scripts/gpu_r04_final.sh (bench20.log: the
+"""Write the live PMC figures of a gpurun_out/<tag> run of scripts/gpu_r06_final.sh (earlier: gpu_r04_final.sh, in git history) (bench20.log: the
 driver's sponza command; bench_bunny.log: the C3 line) into profiles/pmc_traffic.json, keyed by the
 build they were measured on, so that bench.py's profile fallback (--pmc off, N > 1) has them too.
   python scripts/update_pmc_traffic.py TAG"""
