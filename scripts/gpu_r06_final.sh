@@ -26,4 +26,14 @@ timeout -k 10 300 python scripts/level_stats.py --scene bunny --spp 64 > $O/leve
 tail -1 $O/level_stats_bunny.log
 timeout -k 10 400 python scripts/chain_floor.py --scene sponza --n 8 > $O/chain_floor.log 2>&1 || { tail -20 $O/chain_floor.log; exit 1; }
 tail -1 $O/chain_floor.log | cut -c1-600
+if [ "${CONFIGS:-1}" = 1 ]; then
+  timeout -k 10 600 python bench.py --scene cornell --width 1024 --height 1024 --spp 64 --steps 12 --warmup 2 --cpu-rows 4 > $O/c2.log 2>&1 || { tail $O/c2.log; exit 1; }
+  tail -1 $O/c2.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('C2', d['value'], d['ms_per_step'], d['timing']['isolated_launch_ms'], (d.get('cpu_baseline') or {}).get('value'))"
+  timeout -k 10 600 python -m webgputracer_amd.frames --frame 1 48 --spp 64 --batch 4 --pipeline 2 > $O/c5_b4_p2.log 2>&1 || { tail $O/c5_b4_p2.log; exit 1; }
+  echo "C5 $(tail -1 $O/c5_b4_p2.log)"
+  for r in 1 2; do for cn in 2 1; do
+    WGT_CNODE=$cn timeout -k 10 400 python bench.py --scene bunny --steps 20 --warmup 3 --pmc off --no-cpu-baseline --stats-reps 1 > $O/bunny_cn${cn}_$r.log 2>&1 || { tail $O/bunny_cn${cn}_$r.log; exit 1; }
+    echo "bunny cnode=$cn r$r: $(tail -1 $O/bunny_cn${cn}_$r.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['kernel_ms'], d['per_launch']['bvh_nodes'])")"
+  done; done
+fi
 echo done
