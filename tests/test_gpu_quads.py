@@ -60,3 +60,18 @@ def test_quad_ties_trace_rays(ctx, wgt, oracle, kind):
     osc.close()
     assert np.array_equal(gp, rp)
     assert np.array_equal(gd.view(np.uint32), rd.view(np.uint32))
+
+
+def test_traversal_level_counters(ctx, wgt):
+    """The instrumented pass's traversal-by-level counters (round 6, wgt_stats top_node_visits,
+    cyc_node_steps, cyc_top_steps, cyc_tri_steps; scripts/level_stats.py): levels 1-2 hold at most 20
+    of a BVH4's nodes, visits of them are a part of all node visits, and the cycles of steps whose
+    lanes are all at those levels are a part of the node steps' cycles."""
+    L, Q, S, T = wgt.mesh_scene("bunny", 20000)
+    ctx.upload_scene(L, Q, S, T)
+    st = ctx.render_tile(wgt.camera_param(16 / 9, 4, 3), 96, 54, want=("u8",), stats=True)["stats"]
+    assert 0 < st["top_node_visits"] < st["node_visits"]
+    assert 0 <= st["cyc_top_steps"] <= st["cyc_node_steps"] and st["cyc_node_steps"] > 0
+    assert st["cyc_tri_steps"] > 0
+    assert st["cyc_node_steps"] + st["cyc_tri_steps"] <= st["cyc_trav"]
+    assert st["quad_ref_scans"] <= st["traced_rays"]
