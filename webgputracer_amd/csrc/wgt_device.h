@@ -762,7 +762,7 @@ __device__ __forceinline__ bool shade(const DevScene& sc, const Light& L, const 
     return true;
   }
   // sample_direction (path_tracer.wgsl:146-154).  The shading divisions stay IEEE: short forms
-  // behind wave-uniform range tests measured slower
+  // behind per-lane range tests measured slower
   const f3 w = normalize(h.norm);  // onb.w of build_onb_from_w(hit.norm)
   f3 sdir;
   // both branches draw two more rand() (r1 then r2) right away: drawn once here, the
