@@ -227,25 +227,15 @@ template <bool SHORT>
 __device__ __forceinline__ bool tri_test(const float4* __restrict__ tris, uint32_t lf, f3 o, f3 d, f3 ot, f3 inv,
                                          float bt, uint32_t bi, float& tt, uint32_t& idx) {
   const char* __restrict__ p = (const char*)tris + lf;
-  f3 v0, e1, e2, blo, bhi;
-  if (kTriRecordBytes == 64) {
-    // all four float4 of the record at once: the padded box D (for a candidate closest
-    // hit) used to be loaded in the branch, a second dependent round trip
-    const float4 A = ((const float4*)p)[0], B = ((const float4*)p)[1], C = ((const float4*)p)[2],
-                 D = ((const float4*)p)[3];
-    v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
-    idx = __float_as_uint(A.w);
-    blo = f3{B.w, C.w, D.x};
-    bhi = f3{D.y, D.z, D.w};
-  } else {
-    const float4 A = *(const float4*)p, B = *(const float4*)(p + 16);
-    const float2 C = *(const float2*)(p + 32);
-    v0 = xyz(A), e1 = xyz(B), e2 = f3{B.w, C.x, C.y};
-    idx = __float_as_uint(A.w);
-  }
+  // all four float4 of the record at once: the padded box D (for a candidate closest
+  // hit) used to be loaded in the branch, a second dependent round trip
+  const float4 A = ((const float4*)p)[0], B = ((const float4*)p)[1], C = ((const float4*)p)[2],
+               D = ((const float4*)p)[3];
+  const f3 v0 = xyz(A), e1 = xyz(B), e2 = xyz(C);
+  idx = __float_as_uint(A.w);
+  const f3 blo = f3{B.w, C.w, D.x}, bhi = f3{D.y, D.z, D.w};
   if (!mt_test<SHORT>(o, d, v0, e1, e2, tt)) return false;
   if (!(tt < bt || (tt == bt && idx < bi))) return false;
-  if (kTriRecordBytes != 64) tri_box(v0, e1, e2, blo, bhi);
   float bn, bf;
   slab(ot, inv, blo, bhi, bn, bf);
   return bn <= tt && tt <= bf;
@@ -493,7 +483,7 @@ using Stack24 = Stack24S<>;
 // needs no scratch.  Word 9 holds the LDS stack top in its low half and the depth of the
 // lane's global stack (entries moved out of LDS, DevFrame::ps_spill) in its high half:
 // the traversal phase reads and writes only the low half.  The open leaf is one word:
-// the record offset (a multiple of kTriRecordBytes = 64) plus the records left (<= 8).
+// the record offset (a multiple of kTriRecordBytes) plus the records left (<= 8).
 struct Park {
   uint32_t* __restrict__ p;
   __device__ __forceinline__ uint32_t ld(int j) const { return p[j * kBlock]; }
@@ -501,11 +491,14 @@ struct Park {
   __device__ __forceinline__ uint32_t sp() const { return ((const uint16_t*)(p + 9 * kBlock))[0]; }
   __device__ __forceinline__ void set_sp(uint32_t v) const { ((uint16_t*)(p + 9 * kBlock))[0] = (uint16_t)v; }
 };
-static_assert(kTriRecordBytes == 64, "the parked open leaf packs its count into the offset's low 6 bits");
+// the record offset's zero low bits (6 for 64-B records) hold the count (<= kLeafMax)
+constexpr uint32_t kParkLeafMask = kTriRecordBytes - 1u;
+static_assert((kTriRecordBytes & kParkLeafMask) == 0u && kParkLeafMask >= (uint32_t)kLeafMax,
+              "the parked open leaf packs its count into the offset's low bits");
 __device__ __forceinline__ uint32_t park_leaf(const Trav& t) { return t.lf | ((t.le - t.lf) / kTriRecordBytes); }
 __device__ __forceinline__ void unpark_leaf(uint32_t w, Trav& t) {
-  t.lf = w & ~63u;
-  t.le = t.lf + (w & 63u) * kTriRecordBytes;
+  t.lf = w & ~kParkLeafMask;
+  t.le = t.lf + (w & kParkLeafMask) * kTriRecordBytes;
 }
 // the whole state; the global depth (word 9's high half) is left as it is
 __device__ __forceinline__ void park_put(const Park& P, const Trav& t) {

@@ -101,19 +101,15 @@ WGT_HD bool mt_test(f3 o, f3 d, f3 v0, f3 e1, f3 e2, float& tout) {
 // Leaf-ordered triangle record, 64 B (4 x float4), one cache-line half:
 //   A = (v0.xyz, original index bits)   B = (e1.xyz, box.lo.x)
 //   C = (e2.xyz, box.lo.y)              D = (box.lo.z, box.hi.xyz)
-// A-C feed Moller-Trumbore; D (same 128-B line) is read only for a candidate
-// closest hit, to check t against the triangle's own padded box (tri_box,
+// A-C feed Moller-Trumbore; D (same 128-B line, loaded with A-C) is used only for a
+// candidate closest hit, to check t against the triangle's own padded box (tri_box,
 // computed by the host builder with the same fp32 operations).
 constexpr int kTriRecordFloats = 16;  // the host / exported record (wgt_bvh_build)
-// The device record the kernels walk (by byte offsets): the 64-B record above, or with
-// WGT_TRI_REC=40 a 40-B one, (v0, index), (e1, e2.x), (e2.y, e2.z), whose padded box is
-// recomputed (tri_box, the builder's own fp32 operations: the same bits) for a
-// candidate closest hit only.
-#ifndef WGT_TRI_REC
-#define WGT_TRI_REC 64
-#endif
-static_assert(WGT_TRI_REC == 64 || WGT_TRI_REC == 40, "triangle record: 64 or 40 bytes");
-constexpr uint32_t kTriRecordBytes = WGT_TRI_REC;
+// The device record the kernels walk (by byte offsets) is the 64-B record above.  Records
+// without the padded box (40 B, round 3; 48 B with 16-B aligned loads, round 6) load one
+// float4 fewer per test but recompute the box (tri_box) for a candidate: slower on both
+// scenes, removed.
+constexpr uint32_t kTriRecordBytes = 64;
 // triangles tested per triangle step of the phase-split kernel (wgt_device.h tri_step): two
 // measured -1.6% on sponza, -1.3% on bunny at 1080p/256 spp; three and four +6%/+13% on sponza
 // (profiles/sweeps/r03_ab_tri_per_step.log)

@@ -233,7 +233,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
         // entries to or from its global stack and traverses on
         bool resume = false;
         if (PK && TRIS && pending && !nanray) {
-          resume = (int)P.ld(8) != kNoRef || (P.ld(10) & 63u) != 0u || P.ld(9) != 0u;
+          resume = (int)P.ld(8) != kNoRef || (P.ld(10) & kParkLeafMask) != 0u || P.ld(9) != 0u;
           if (resume) {
             // the lane's global stack: entry e at gs[e * fr.ps_spill_stride]
             const uint32_t k = park_fix(sc, P, lds, cap, spill + blockIdx.x * kBlock + lane, fr.ps_spill_stride);

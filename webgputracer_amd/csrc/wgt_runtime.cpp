@@ -623,21 +623,9 @@ int wgt_upload_scene(wgt_ctx* ctx, const wgt_quad* lights, uint32_t n_lights, co
       if (r >= 0 && (size_t)r < bvh.n_nodes) level[r] = (uint8_t)std::min(255, level[i] + 1);
     }
   const size_t b_level = align256(level.size());
-  // the device triangle records (wgt_geom.h kTriRecordBytes): the builder's 64-B records,
-  // or their 40-B form without the padded box
-  std::vector<float> dtris;
-  if (kTriRecordBytes == 64) {
-    dtris = bvh.tris;
-  } else {
-    dtris.resize((size_t)n_tris * (kTriRecordBytes / 4));
-    for (size_t i = 0; i < n_tris; ++i) {
-      const float* a = &bvh.tris[i * kTriRecordFloats];
-      float* o = &dtris[i * (kTriRecordBytes / 4)];
-      o[0] = a[0]; o[1] = a[1]; o[2] = a[2]; o[3] = a[3];     // v0, index bits
-      o[4] = a[4]; o[5] = a[5]; o[6] = a[6];                  // e1
-      o[7] = a[8]; o[8] = a[9]; o[9] = a[10];                 // e2
-    }
-  }
+  // the device triangle records (wgt_geom.h kTriRecordBytes): the builder's 64-B records
+  static_assert(kTriRecordBytes == kTriRecordFloats * 4, "device and host triangle records");
+  const std::vector<float>& dtris = bvh.tris;
   const size_t b_tris = align256(dtris.size() * 4);
   const size_t b_shade = align256(bvh.tshade.size() * 4);
   const uint32_t waves = ps_waves_for(bvh, n_tris);
