@@ -212,9 +212,9 @@ def test_compact_nodes_wide_and_tiny_extents():
 
 
 def test_compact_nodes_full_size_meshes():
-    """Auto rule: the bunny stand-in's 128-B tree (2.3 MB) fits one XCD's 4 MB L2 and
-    keeps the 128-B nodes; sponza's (8.5 MB) does not, so the persistent kernel reads
-    the compact form."""
+    """The size rule (scene_info bvh_compact; WGT_CNODE=2 reads the node form by it): the bunny
+    stand-in's 128-B tree (2.3 MB) fits one XCD's 4 MB L2, sponza's (8.5 MB) does not.  The
+    default (WGT_CNODE=1) reads the compact form for both."""
     for kind, compact in (("bunny", 0), ("sponza", 1)):
         tris = w.procedural_mesh(kind)
         assert check_compact(tris)["bvh_compact"] == compact

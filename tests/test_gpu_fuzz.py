@@ -2,7 +2,7 @@
 test covers — random lights, quads (any orientation, some emissive), spheres (the last one emissive
 or not), triangle soups and cameras placed anywhere in and around the Cornell box's extent.
 
-Each scene is rendered by the persistent kernel (its default schedule, then the compact node form
+Each scene is rendered by the persistent kernel (its default schedule, then the 128-B node form
 and block order) and by the simple kernel; every radiance word, hit ID and exact counter must equal
 the oracle's.  The records' derived fields (quad normal, w, d; triangle edges and face normal) are
 computed in numpy fp32: parity compares the two implementations on the same input bytes, whatever
@@ -78,7 +78,7 @@ def test_random_scene_parity(ctx, wgt, oracle, seed, monkeypatch):
     osc = oracle.OracleScene(L, Q, S, T)
     r = osc.render(cam_o, W, H)
     osc.close()
-    for env in ({}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_KERNEL": "1"}):
+    for env in ({}, {"WGT_CNODE": "0", "WGT_PQ_LPT": "0"}, {"WGT_KERNEL": "1"}):
         for k in ("WGT_CNODE", "WGT_PQ_LPT", "WGT_KERNEL"):
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():

@@ -74,7 +74,7 @@ def test_scaled_cornell_vs_oracle(ctx, wgt, oracle, log2s):
 @pytest.mark.parametrize("log2s", [-60, -8, 20])
 def test_scaled_mesh_vs_oracle(ctx, wgt, oracle, log2s, cnode, monkeypatch):
     """The BVH path (a 2k-triangle mesh in the Cornell walls) at the same scales, on the
-    auto node form (128-B nodes for this small tree) and forced onto the compact nodes,
+    size rule's node form (WGT_CNODE=2: 128-B nodes for this small tree) and on the compact nodes,
     whose fused slab step relies on the builder's code margin."""
     monkeypatch.setenv("WGT_CNODE", cnode)
     s = 2.0 ** log2s

@@ -260,8 +260,8 @@ def _sponza(wgt, oracle):
 
 @pytest.mark.parametrize("cnode", ["2", "0", "1"])
 def test_sponza_render_parity(ctx, wgt, oracle, cnode, monkeypatch):
-    """Sponza stand-in: by default (2) the persistent kernel reads the 80-B compact records
-    (the 128-B tree exceeds one XCD's L2), 0 forces the 128-B nodes, 1 the compact records."""
+    """Sponza stand-in: the persistent kernel reads the 80-B compact records by default (1) and by
+    the size rule (2: the 128-B tree exceeds one XCD's L2); 0 forces the 128-B nodes."""
     monkeypatch.setenv("WGT_CNODE", cnode)
     L, Q, S, T = _sponza(wgt, oracle)
     ctx.upload_scene(L, Q, S, T)
@@ -281,11 +281,11 @@ _FULL = {}
 
 @pytest.mark.parametrize("kind,spp,env", [("sponza", 4, {}), ("sponza", 4, {"WGT_CNODE": "0"}),
                                           ("sponza", 4, {"WGT_PARK": "1"}), ("bunny", 1, {}),
-                                          ("bunny", 1, {"WGT_CNODE": "1"})])
+                                          ("bunny", 1, {"WGT_CNODE": "0"})])
 def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatch):
     """Every pixel of a full 1920x1080 frame at the bench's resolution, GPU vs the
-    oracle (OpenMP), through the default kernel of each scene: sponza on the 80-B compact
-    records, bunny on the 128-B nodes, both at 6 waves/SIMD with 3-byte stack entries; and each
+    oracle (OpenMP), through the default kernel of each scene: both on the 80-B compact
+    records (round 6; until then bunny read the 128-B nodes), at 6 waves/SIMD with 3-byte stack entries; and each
     on the other node form, and sponza with parked traversal state (WGT_PARK=1, an 18-entry LDS
     stack)."""
     for k, v in env.items():
@@ -296,6 +296,7 @@ def test_full_frame_1080p_bit_exact(ctx, wgt, oracle, kind, spp, env, monkeypatc
     if not any(os.environ.get(k) for k in ("WGT_CNODE", "WGT_PS_WAVES", "WGT_STACK_LIMIT", "WGT_PARK")):
         assert (info["bvh_compact"], info["ps_waves"]) == ((1, 6) if kind == "sponza" else (0, 6))
         assert info["ps_park"] == 0 and info["ps_stack"] == info["bvh_stack"] + 1
+        assert info["node_form"] == 1
     g = ctx.render_tile(wgt.camera_param(16 / 9, spp, 3), 1920, 1080, stats=True)
     if kind not in _FULL:
         osc = oracle.OracleScene(L, Q, S, T)
@@ -344,29 +345,29 @@ _SCHED_REF = {}
                                  {"WGT_PS_SVC_FRAC": "1"},
                                  # the cost pre-pass's path depth (default 6): its shortest and the full path
                                  {"WGT_PQ_DEPTH": "1"}, {"WGT_PQ_DEPTH": "50"},
-                                 {"WGT_CNODE": "1"}, {"WGT_CNODE": "1", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
-                                 {"WGT_PS_WAVES": "5", "WGT_CNODE": "1"}, {"WGT_NARROW": "1"},
+                                 {"WGT_CNODE": "0"}, {"WGT_CNODE": "0", "WGT_PQ_LPT": "0"}, {"WGT_PS_WAVES": "5"},
+                                 {"WGT_PS_WAVES": "5", "WGT_CNODE": "0"}, {"WGT_NARROW": "1"},
                                  {"WGT_STACK_LIMIT": "20"},
                                  # parked traversal state (WGT_PARK=1): the default LDS stack, the
                                  # smallest (every node step near the top spills to the global stack),
                                  # per node form and wave budget
-                                 {"WGT_PARK": "1"}, {"WGT_PARK": "1", "WGT_CNODE": "1"},
-                                 {"WGT_PARK": "1", "WGT_PS_CAP": "8"}, {"WGT_PARK": "1", "WGT_PS_CAP": "8", "WGT_CNODE": "1"},
+                                 {"WGT_PARK": "1"}, {"WGT_PARK": "1", "WGT_CNODE": "0"},
+                                 {"WGT_PARK": "1", "WGT_PS_CAP": "8"}, {"WGT_PARK": "1", "WGT_PS_CAP": "8", "WGT_CNODE": "0"},
                                  {"WGT_PARK": "1", "WGT_PS_CAP": "8", "WGT_PS_WAVES": "5"},
                                  {"WGT_PARK": "1", "WGT_PS_CAP": "9", "WGT_PQ_LPT": "0"},
                                  # triangle steps as soon as one lane has a leaf open (1), or node steps
                                  # while any lane has a node (the most second leaves parked on the stack)
                                  {"WGT_TRI_RATIO": "1"}, {"WGT_TRI_RATIO": "1000000"},
-                                 {"WGT_TRI_RATIO": "1", "WGT_CNODE": "1"},
+                                 {"WGT_TRI_RATIO": "1", "WGT_CNODE": "0"},
                                  ])
 def test_ps_schedule_invariance(ctx, wgt, oracle, bunny, env, monkeypatch):
     """The persistent phase-split kernel's scheduling knobs (queue order: LPT from the
     cost pre-pass (1 or 4 spp) or block order; refill threshold; phase thresholds and
-    their sparse-wave scaling; the node form: compact nodes forced on the bunny; the
+    their sparse-wave scaling; the node form: 128-B nodes forced on the bunny; the
     wave budget: 6 waves per SIMD with 3-byte stack entries or, with WGT_PS_WAVES=5, 5
     with 4-byte ones; the narrow 25-entry tree, WGT_NARROW=1; a 20-entry bound, which moves
     the 3-byte stack's byte array; the parked traversal state with small LDS stacks,
-    WGT_PARK=1 with LDS stacks down to WGT_PS_CAP=8; 7 waves per SIMD)
+    WGT_PARK=1 with LDS stacks down to WGT_PS_CAP=8)
     change which lane renders which pixel and when, never a bit of the result.  100x60
     leaves ragged 8x8 blocks at the frame edge.  The test runs after the kernel-family
     tests on the same context, the sequence that exposed a workspace-reuse bug (each

@@ -583,10 +583,11 @@ void ps_launch(const DevScene& sc, int cn, dim3 grid, dim3 block, size_t lds, hi
 
 // The compact codes are exact for ray origins within their bound (the margin, wgt_geom.h):
 // hit points always are, the camera is checked per frame (beyond: the 128-B nodes).
-// WGT_CNODE: 0 = 128-B, 1 = 80-B, 2 = 80-B when the 128-B tree would not fit one XCD's
-// 4 MB L2 (sponza stand-in: 7.3 MB -> 4.6 MB; default).  A tree that fits keeps the 128-B nodes,
-// whose step needs fewer VALU.  (Round 6 removed the 64-B records, WGT_CNODE=3,
-// and the wide 8-slot records, WGT_CNODE=4: slower on every measured scene)
+// WGT_CNODE: 0 = 128-B, 1 = 80-B (default), 2 = 80-B when the 128-B tree would not fit one XCD's
+// 4 MB L2 (sponza stand-in: 7.3 MB -> 4.6 MB; the default until round 6, when the compact step's
+// integer bound minimum made the 80-B records faster on the bunny's L2-resident tree too, +0.6 %,
+// DESIGN.md §4.2 item 30).  (Round 6 removed the 64-B records, WGT_CNODE=3, and the wide 8-slot
+// records, WGT_CNODE=4: slower on every measured scene)
 int node_form(const DevScene& sc, const DevFrame& fr) {
   const float cam = fmaxf(fmaxf(fabsf(fr.ox), fabsf(fr.oy)), fabsf(fr.oz));
   if (!(cam <= sc.cbound)) return 0;

@@ -207,7 +207,7 @@ DevFrame make_frame(const wgt_camera_param& cam, uint32_t W, uint32_t H) {
   fr.ps_svc_frac = env_u32("WGT_PS_SVC_FRAC", 16);  // sweep: profiles/sweeps/r01_ps_svc_frac.jsonl
   // >= 1: with 0 a wave whose lanes all hold a node but no open leaf would take triangle steps forever
   fr.tri_ratio = std::max<uint32_t>(env_u32("WGT_TRI_RATIO", 100), 1u);
-  fr.cnode = env_u32("WGT_CNODE", 2);  // compact nodes once the 128-B tree outgrows an XCD's L2
+  fr.cnode = env_u32("WGT_CNODE", 1);  // compact nodes (2: only once the 128-B tree outgrows an XCD's L2)
   fr.pq_refill = env_u32("WGT_PQ_REFILL", 0);  // 0 = the default, 2 (launch_render)
   // 0: block order (A/B); n: LPT order from an n*n-spp cost pre-pass (when spp > n*n)
   fr.pq_lpt = env_u32("WGT_PQ_LPT", 1);
