@@ -200,7 +200,7 @@ k_render_ps(DevScene sc, DevFrame fr, const wgt_tile* __restrict__ tiles, uchar4
           const int leader = __ffsll((long long)idle) - 1;
           uint32_t base = 0;
           if ((int)lane == leader) base = atomicAdd(queue, n_idle);
-          base = __shfl(base, leader);
+          base = __builtin_amdgcn_readlane(base, leader);  // leader is wave-uniform: no lane index, no LDS
           if (!have && !exhausted) {
             // the lane's rank among the idle lanes (mbcnt: the set bits of idle below this lane)
             const uint32_t slot = base + __builtin_amdgcn_mbcnt_hi((uint32_t)(idle >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)idle, 0u));
