@@ -218,24 +218,11 @@ __device__ __forceinline__ void simt_count(uint32_t& wave, uint32_t& lane) {
   ++lane;
 }
 
-// One triangle test of the record at byte offset lf (wgt_geom.h kTriRecordBytes):
+// One triangle test of a 64-B record (wgt_geom.h kTriRecordBytes) held in registers:
 // Moller-Trumbore, then for a candidate that beats (bt, bi) the slab check against the
 // triangle's own padded box.  inv: 1/d.  Returns true with (tt, idx)
 // when the triangle becomes the closest hit.
 // SHORT: mt_test's short reciprocal (render rays only, wgt_geom.h).
-template <bool SHORT>
-__device__ __forceinline__ bool tri_test_rec(float4 A, float4 B, float4 C, float4 D, f3 o, f3 d, f3 ot, f3 inv,
-                                             float bt, uint32_t bi, float& tt, uint32_t& idx);
-template <bool SHORT>
-__device__ __forceinline__ bool tri_test(const float4* __restrict__ tris, uint32_t lf, f3 o, f3 d, f3 ot, f3 inv,
-                                         float bt, uint32_t bi, float& tt, uint32_t& idx) {
-  const char* __restrict__ p = (const char*)tris + lf;
-  // all four float4 of the record at once: the padded box D (for a candidate closest
-  // hit) used to be loaded in the branch, a second dependent round trip
-  const float4 A = ((const float4*)p)[0], B = ((const float4*)p)[1], C = ((const float4*)p)[2],
-               D = ((const float4*)p)[3];
-  return tri_test_rec<SHORT>(A, B, C, D, o, d, ot, inv, bt, bi, tt, idx);
-}
 template <bool SHORT>
 __device__ __forceinline__ bool tri_test_rec(float4 A, float4 B, float4 C, float4 D, f3 o, f3 d, f3 ot, f3 inv,
                                              float bt, uint32_t bi, float& tt, uint32_t& idx) {
@@ -247,6 +234,14 @@ __device__ __forceinline__ bool tri_test_rec(float4 A, float4 B, float4 C, float
   float bn, bf;
   slab(ot, inv, blo, bhi, bn, bf);
   return bn <= tt && tt <= bf;
+}
+// The same for the record at byte offset lf: all four float4 loaded at once (the padded box D,
+// for a candidate closest hit, used to be loaded in the branch, a second dependent round trip).
+template <bool SHORT>
+__device__ __forceinline__ bool tri_test(const float4* __restrict__ tris, uint32_t lf, f3 o, f3 d, f3 ot, f3 inv,
+                                         float bt, uint32_t bi, float& tt, uint32_t& idx) {
+  const float4* __restrict__ p = (const float4*)((const char*)tris + lf);
+  return tri_test_rec<SHORT>(p[0], p[1], p[2], p[3], o, d, ot, inv, bt, bi, tt, idx);
 }
 
 // Resumable BVH4 traversal: closest triangle = min (t, index) with t < bound (or
